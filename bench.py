@@ -1,0 +1,205 @@
+"""Benchmark: Mrays/s of the sphere-cave frame fill on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A step is one full frame: every rank fills its row band of a 3840 x (2160*N)
+RGBA8 frame in HBM through libsfrt.so (64-sphere cave, BASELINE config 3),
+then for N > 1 the bands are gathered to rank 0 over RCCL.  Per-GPU work is
+fixed as N grows ("weak" scaling); rays use the global row index, so the
+gathered frame is byte-identical to a single-GPU render of the same frame.
+value = all rays of the K frames / (max over ranks of the timed wall time).
+
+Also reported (rank 0, N = 1): the 1920x1080 10-sphere frame (BASELINE
+config 2), the kernel's HBM roofline from HIP events on the launch stream,
+and the CPU baseline: the oracle (CPU restatement, oracle/) rendering one
+whole 4K frame on the host cores, compared byte for byte with the GPU frame.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import scenes  # noqa: E402
+import sfrt  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_VALU_PEAK_TFLOPS = 157.3
+BYTES_PER_RAY = 4            # RGBA8 store; texture + sphere table are cache-resident
+WIDTH, ROWS_PER_GPU = 3840, 2160
+
+
+def band_of(rank: int, world: int, height: int) -> tuple[int, int]:
+    r0 = rank * height // world
+    return r0, (rank + 1) * height // world - r0
+
+
+def time_frames(world, buf, pitch, row0, rows, steps, warmup, stream, gather=None):
+    """Warmup, then `steps` timed frames.  Returns (wall seconds, kernel ms per frame)."""
+    for _ in range(warmup):
+        world.render_band(buf.data_ptr(), pitch, row0, rows, stream.cuda_stream)
+        if gather:
+            gather()
+    world.check(stream.cuda_stream)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        starts[k].record(stream)
+        world.render_band(buf.data_ptr(), pitch, row0, rows, stream.cuda_stream)
+        ends[k].record(stream)
+        if gather:
+            gather()
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    world.check(stream.cuda_stream)
+    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
+    return wall, kernel_ms
+
+
+def cpu_baseline(scene, width, height, floor, gpu_frame):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU restatement, timed as the baseline
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = oracle.Oracle.from_scene(scene, width, height, *floor)
+    t0 = time.perf_counter()
+    frame = o.render(threads)
+    dt = time.perf_counter() - t0
+    same = bool(np.array_equal(frame, gpu_frame))
+    return {"value": round(width * height / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+            "kind": "port",
+            "sample": f"one full {width}x{height} frame of the same scene, oracle/sphereworld_oracle.c "
+                      f"(-O2, no FMA), {threads} threads with the reference's row interleave "
+                      f"(Source.cpp:21), {dt:.2f} s",
+            "frame_bit_identical_to_gpu": same}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    torch.cuda.set_device(local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    floor = scenes.load_floor()
+    scene = scenes.lcg64()
+    height = ROWS_PER_GPU * world_size
+    row0, rows = band_of(rank, world_size, height)
+    pitch = WIDTH * 4
+    # A dedicated stream: the kernels, the HIP events that time them and the
+    # RCCL gather (which orders itself after the current stream) all use it.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    w = sfrt.World(local_rank)
+    w.load_texture(*floor)
+    w.set_scene(scene, WIDTH, height)
+
+    if world_size > 1:
+        band_rows = [band_of(r, world_size, height)[1] for r in range(world_size)]
+        if rank == 0:
+            frame = torch.empty(height, pitch, dtype=torch.uint8, device="cuda")
+            buf = frame[row0:row0 + rows]
+            gather_list = [frame[band_of(r, world_size, height)[0]:][:band_rows[r]]
+                           for r in range(world_size)]
+        else:
+            buf = torch.empty(rows, pitch, dtype=torch.uint8, device="cuda")
+            gather_list = None
+
+        def gather():
+            dist.gather(buf, gather_list, dst=0)
+    else:
+        buf = torch.empty(rows, pitch, dtype=torch.uint8, device="cuda")
+        gather = None
+
+    wall, kernel_ms = time_frames(w, buf, pitch, row0, rows, args.steps, args.warmup, stream,
+                                  gather)
+    if world_size > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    total_rays = WIDTH * height * args.steps
+    value = total_rays / wall / 1e6
+    ms_per_step = wall / args.steps * 1e3
+
+    result = None
+    if rank == 0:
+        rays_per_launch = WIDTH * rows
+        achieved = BYTES_PER_RAY * rays_per_launch / (kernel_ms * 1e-3) / 1e9
+        result = {
+            "metric": "Mrays/s (primary rays, full RGBA8 frames in HBM)",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "fps": round(1e3 / ms_per_step, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: pinned 64-sphere cave (SURVEY 8d config 3), Floor.png texels",
+            "config": {"workload": f"{WIDTH}x{height} lcg64 pose(0,0), {world_size} row band(s)"
+                                   + (" + RCCL gather to rank 0" if world_size > 1 else ""),
+                       "width": WIDTH, "height": height, "spheres": int(scene.spheres.shape[0]),
+                       "parallelism": f"row-bands x{world_size}"},
+            "kernel_ms": round(kernel_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": None,
+                         "note": "algorithmic bytes = 4 B/ray (RGBA8 store) x rays per launch / "
+                                 "kernel time (HIP events on the launch stream); the kernel is "
+                                 "VALU-bound, see DESIGN.md"},
+        }
+    if world_size == 1:
+        # BASELINE config 2: 1920x1080, 10-sphere scene.
+        w2 = sfrt.World(local_rank)
+        w2.load_texture(*floor)
+        w2.set_scene(scenes.default10(), 1920, 1080)
+        buf2 = torch.empty(1080, 1920 * 4, dtype=torch.uint8, device="cuda")
+        wall2, k2 = time_frames(w2, buf2, 1920 * 4, 0, 1080, args.steps, args.warmup, stream)
+        result["also"] = {"1920x1080_default10": {
+            "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
+            "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4)}}
+        w2.close()
+        if not args.no_cpu_baseline:
+            torch.cuda.synchronize()
+            gpu_frame = buf.cpu().numpy().ravel()
+            result["cpu_baseline"] = cpu_baseline(scene, WIDTH, height, floor, gpu_frame)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    w.close()
+    if world_size > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

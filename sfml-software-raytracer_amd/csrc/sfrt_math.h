@@ -1,0 +1,187 @@
+// sfrt_math.h -- bit-exact binary32 atanf / atan2f / asinf for host and device.
+//
+// The reference shades every pixel with std::atan2(float, float) and
+// std::asinf (/root/reference/Raytracing/SphereWorld.cpp:326 via :373, and
+// :374), i.e. the host libm's atan2f / asinf.  The device libm (OCML) uses
+// different polynomials, so the kernel cannot call it and stay bit-exact.
+// These functions restate the algorithm of glibc 2.35's float versions, which
+// are the fdlibm-derived sysdeps/ieee754/flt-32/{s_atanf,e_atan2f,e_asinf}.c
+// (no IFUNC variants on x86-64: `nm -D libm.so.6` shows plain W symbols).
+// Constants are the exact binary32 values glibc uses (read from its .rodata;
+// they equal fdlibm's published ones), and the operation order follows the
+// compiled code, so the results are the same on any IEEE-754 binary32 target
+// that evaluates without contraction.  tests/test_math_exhaustive.py checks
+// them against the host libm over every binary32 input of atanf/asinf and
+// ~10^8 atan2f pairs; tests/test_gpu_parity.py repeats that on gfx950.
+//
+// REQUIREMENTS: compile with -ffp-contract=off, no -ffast-math, and (device)
+// correctly rounded fp32 division and sqrt (hipcc's default).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SFRT_HD __host__ __device__ __forceinline__
+#else
+#define SFRT_HD static inline
+#endif
+
+#pragma clang fp contract(off)
+
+namespace sfrt_math {
+
+SFRT_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+SFRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// s_atanf.c
+SFRT_HD float atanf(float x) {
+  const uint32_t hx = f2u(x);
+  const uint32_t ix = hx & 0x7fffffffu;
+  if (ix >= 0x4c000000u) {               // |x| >= 2^25 (or NaN / inf)
+    if (ix > 0x7f800000u) return x + x;  // NaN
+    if ((int32_t)hx > 0) return u2f(0x33a22168u) + u2f(0x3fc90fdau);  // atanlo[3] + atanhi[3]
+    return u2f(0xbfc90fdau) - u2f(0x33a22168u);                        // -atanhi[3] - atanlo[3]
+  }
+  int id;
+  if (ix < 0x3ee00000u) {                // |x| < 0.4375
+    if (ix < 0x31000000u) return x;      // |x| < 2^-29: huge + x > one holds
+    id = -1;
+  } else {
+    x = u2f(ix);                         // fabsf
+    if (ix < 0x3f980000u) {              // |x| < 1.1875
+      if (ix < 0x3f300000u) {            // 7/16 <= |x| < 11/16
+        id = 0;
+        x = ((x + x) - 1.0f) / (x + 2.0f);
+      } else {                           // 11/16 <= |x| < 19/16
+        id = 1;
+        x = (x - 1.0f) / (x + 1.0f);
+      }
+    } else {
+      if (ix < 0x401c0000u) {            // |x| < 2.4375
+        id = 2;
+        x = (x - 1.5f) / (x * 1.5f + 1.0f);
+      } else {                           // 2.4375 <= |x| < 2^25
+        id = 3;
+        x = -1.0f / x;
+      }
+    }
+  }
+  const float z = x * x;
+  const float w = z * z;
+  // aT[0,2,..,10] (odd-power terms) and aT[1,3,..,9] (even-power terms)
+  float s1 = u2f(0x3c8569d7u) * w + u2f(0x3d4bda59u);   // aT10*w + aT8
+  s1 = s1 * w + u2f(0x3d886b35u);                      // aT6
+  s1 = s1 * w + u2f(0x3dba2e6eu);                      // aT4
+  s1 = s1 * w + u2f(0x3e124925u);                      // aT2
+  s1 = s1 * w + u2f(0x3eaaaaabu);                      // aT0
+  s1 = s1 * z;
+  float s2 = u2f(0xbd15a221u) * w - u2f(0x3d6ef16bu);   // aT9*w + aT7
+  s2 = s2 * w - u2f(0x3d9d8795u);                      // aT5
+  s2 = s2 * w - u2f(0x3de38e38u);                      // aT3
+  s2 = s2 * w - u2f(0x3e4ccccdu);                      // aT1
+  s2 = s2 * w;
+  const float xs = (s1 + s2) * x;
+  if (id < 0) return x - xs;
+  float hi, lo;
+  switch (id) {
+    case 0: hi = u2f(0x3eed6338u); lo = u2f(0x31ac3769u); break;
+    case 1: hi = u2f(0x3f490fdau); lo = u2f(0x33222168u); break;
+    case 2: hi = u2f(0x3f7b985eu); lo = u2f(0x33140fb4u); break;
+    default: hi = u2f(0x3fc90fdau); lo = u2f(0x33a22168u); break;
+  }
+  const float r = hi - ((xs - lo) - x);
+  return (int32_t)hx < 0 ? -r : r;
+}
+
+// e_atan2f.c
+SFRT_HD float atan2f(float y, float x) {
+  const float tiny = u2f(0x0da24260u);    // 1.0e-30
+  const float pi_o_4 = u2f(0x3f490fdbu);
+  const float pi_o_2 = u2f(0x3fc90fdbu);
+  const float pi = u2f(0x40490fdbu);
+  const float m_pi_lo = u2f(0x33bbbd2eu); // -pi_lo = 8.7422776573e-08
+  const uint32_t hx = f2u(x), hy = f2u(y);
+  const uint32_t ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
+  if (ix > 0x7f800000u || iy > 0x7f800000u) return x + y;  // NaN
+  if (hx == 0x3f800000u) return sfrt_math::atanf(y);       // x == 1.0
+  const int m = (int)((hy >> 31) | ((hx >> 30) & 2u));     // 2*sign(x) + sign(y)
+  if (iy == 0) {
+    switch (m) {
+      case 0:
+      case 1: return y;
+      case 2: return tiny + pi;
+      default: return -pi - tiny;
+    }
+  }
+  if (ix == 0) return (int32_t)hy < 0 ? -pi_o_2 - tiny : tiny + pi_o_2;
+  if (ix == 0x7f800000u) {
+    if (iy == 0x7f800000u) {
+      switch (m) {
+        case 0: return tiny + pi_o_4;
+        case 1: return -pi_o_4 - tiny;
+        case 2: return 3.0f * pi_o_4 + tiny;
+        default: return -3.0f * pi_o_4 - tiny;
+      }
+    }
+    switch (m) {
+      case 0: return 0.0f;
+      case 1: return -0.0f;
+      case 2: return tiny + pi;
+      default: return -pi - tiny;
+    }
+  }
+  if (iy == 0x7f800000u) return (int32_t)hy < 0 ? -pi_o_2 - tiny : tiny + pi_o_2;
+  const int32_t d = (int32_t)iy - (int32_t)ix;
+  const int32_t k = d >> 23;
+  float z;
+  if (d > 0x1e7fffff) {                       // |y/x| > 2^60
+    z = pi_o_2 - u2f(0x333bbd2eu);            // pi_o_2 + 0.5*pi_lo
+  } else if ((int32_t)hx < 0 && k < -60) {    // |y|/x < -2^60
+    z = 0.0f;
+  } else {
+    z = sfrt_math::atanf(u2f(f2u(y / x) & 0x7fffffffu));
+  }
+  switch (m) {
+    case 0: return z;
+    case 1: return u2f(f2u(z) ^ 0x80000000u);
+    case 2: return pi - (z + m_pi_lo);
+    default: return (z + m_pi_lo) - pi;
+  }
+}
+
+// e_asinf.c
+SFRT_HD float asinf(float x) {
+  const float pio2_hi = u2f(0x3fc90fdbu);
+  const float pio2_lo = u2f(0xb33bbd2eu);     // -4.3711388287e-08
+  const float pio4_hi = u2f(0x3f490fdbu);
+  const float p0 = u2f(0x3e2aaae4u), p1 = u2f(0x3d9980f2u), p2 = u2f(0x3d3a3f25u),
+              p3 = u2f(0x3cc6141eu), p4 = u2f(0x3d2cb694u);
+  const uint32_t hx = f2u(x);
+  const uint32_t ix = hx & 0x7fffffffu;
+  if (ix == 0x3f800000u) return x * pio2_lo + x * pio2_hi;  // |x| == 1
+  if (ix > 0x3f800000u) return (x - x) / (x - x);          // |x| > 1: NaN
+  if (ix < 0x3f000000u) {                                 // |x| < 0.5
+    if (ix < 0x32000000u) return x;                       // |x| < 2^-27
+    const float t = x * x;
+    const float w = ((((p4 * t + p3) * t + p2) * t + p1) * t + p0) * t;
+    return x + x * w;
+  }
+  const float w = 1.0f - u2f(ix);
+  const float t = w * 0.5f;
+  const float p = ((((p4 * t + p3) * t + p2) * t + p1) * t + p0) * t;
+  const float s = __builtin_sqrtf(t);
+  float r;
+  if (ix >= 0x3f79999au) {                                // |x| > 0.975
+    const float q = s * p + s;
+    r = pio2_hi - ((q + q) - pio2_lo);
+  } else {
+    const float df = u2f(f2u(s) & 0xfffff000u);
+    const float c = (t - df * df) / (s + df);
+    const float pp = (s + s) * p - (pio2_lo - (c + c));
+    const float q = pio4_hi - (df + df);
+    r = pio4_hi - (pp - q);
+  }
+  return (int32_t)hx > 0 ? r : -r;
+}
+
+}  // namespace sfrt_math

@@ -1,0 +1,72 @@
+// sfrt_trace.h -- per-frame launch record shared by the host mirror
+// (sfrt_world.cpp) and the gfx950 kernels (sphere_trace.hip).
+//
+// Everything that the reference recomputes per pixel but is uniform over the
+// frame is computed once on the host with the reference's own expressions
+// (camera basis SphereWorld.cpp:100-104, ray-angle steps :85-89, the first
+// march iteration from cam.pos, per-sphere atan2f(c.z, c.x) of :326) and
+// shipped here, so the kernel only does per-pixel work.
+#pragma once
+
+#include <stdint.h>
+
+namespace sfrt {
+
+constexpr int kInlineSpheres = 64;    // spheres carried in the kernel-argument segment
+constexpr int kMaxSpheres = 1024;     // 16 culling words of 64 spheres per wave
+constexpr int kMaskWords = kMaxSpheres / 64;
+constexpr int kTile = 8;              // one wave64 = one 8x8 pixel tile
+constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
+constexpr int kMaxIterations = 1 << 20;  // march guard; the reference has none
+
+// One sphere as the kernel reads it: 32 B, one s_load_dwordx8.
+struct SphereRec {
+  float cx, cy, cz, r;
+  float s_pass;    // exact pass threshold: r - sqrtf(s) > 0.01f  <=>  s < s_pass
+  float atan_c;    // atan2f(cz, cx), the centre term of VAngleXZ (SphereWorld.cpp:326)
+  float pad0, pad1;
+};
+
+struct FrameRec {
+  float cam[3];
+  float fwd[3], right[3], up[3];   // basis after VRotateX/VRotateY (SphereWorld.cpp:100-104)
+  float h_start, h_inc, v_start, v_inc;  // SphereWorld.cpp:85-89
+  float first_l;                    // largestDist of the first march iteration (pos == cam)
+  int first_draw;                   // drawSphere after the first iteration
+  int n;                            // sphere count
+  int width, height;                // global frame (bounds for the subset walk)
+  int xstart, xadd, ystart, yadd;   // UpdateImage pixel subset (SphereWorld.cpp:94,97)
+  int sub_w;                        // columns in the subset
+  int sub_row0, sub_rows;           // subset rows rendered by this launch
+  int tiles_x;                      // ceil(sub_w / 8)
+  int tex_w, tex_h;
+  float tex_wf, tex_hf;             // (float)texsize.x / .y (SphereWorld.cpp:376-377)
+  int cull;                         // 1: per-wave cone culling (default), 0: every sphere
+  long long out_pitch;              // output pitch in pixels
+  uint32_t* out;                    // pixel (a, b) -> out[(b - sub_row0) * out_pitch + a]
+  const uint32_t* tex;              // RGBA8 texels
+  const SphereRec* spheres;         // device copy (used when n > kInlineSpheres)
+  int* status;                      // device word: bit 0 = march guard hit, bit 1 = bad texel
+};
+
+// Kernel argument for n <= kInlineSpheres: frame + spheres in the kernarg segment.
+struct InlineArgs {
+  FrameRec f;
+  SphereRec s[kInlineSpheres];
+};
+
+struct PixelDump {
+  float pos[3];
+  int draw;
+  int iters;
+  float xcoord, ycoord, brightness;
+  uint32_t texel[2];
+  uint32_t rgba;
+};
+
+// sphere_trace.hip
+int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream);
+int launch_trace_points(const FrameRec& f, const int* dev_ij, int count, PixelDump* dev_out,
+                        void* stream);
+
+}  // namespace sfrt

@@ -1,0 +1,538 @@
+// sfrt_world.cpp -- host side of the drop-in: a C++ mirror of the scene state
+// that SphereWorld::UpdateImage reads, the per-frame preparation the kernel
+// needs, and the extern "C" boundary declared in include/sfrt.h.
+//
+// Reference interface mirrored (paths under /root/reference/Raytracing/):
+//   SphereWorld::width/height/cam     SphereWorld.h:50-52 (defaults 320x180, fov 75/47 deg)
+//   SphereWorld::SphereWorld          SphereWorld.cpp:43-77 (fov -> radians :72-73)
+//   SphereWorld::AddSphere            SphereWorld.cpp:177-190
+//   SphereWorld::UpdateSpheres (sort) SphereWorld.cpp:199-212
+//   SphereWorld::UpdateImage          SphereWorld.cpp:83-112
+//   textures[0]                       SphereWorld.h:74, SphereWorld.cpp:52
+// Compiled with -ffp-contract=off: every float expression below is
+// evaluated exactly as the reference writes it.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "sfrt.h"
+#include "sfrt_math.h"
+#include "sfrt_trace.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kPI = 3.1415926535f;  // SphereWorld.h:6
+
+struct V3 {
+  float x, y, z;
+};
+inline V3 vsub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+// SphereWorld.cpp:340-343
+inline float vlength(V3 v) { return std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }
+// SphereWorld.cpp:27-31
+inline V3 rot_x(V3 v, float amount) {
+  const float s = std::sin(amount);
+  const float c = std::cos(amount);
+  return {v.x, v.y * c - v.z * s, v.y * s + v.z * c};
+}
+// SphereWorld.cpp:32-36
+inline V3 rot_y(V3 v, float amount) {
+  const float s = std::sin(amount);
+  const float c = std::cos(amount);
+  return {v.x * c + v.z * s, v.y, -v.x * s + v.z * c};
+}
+inline V3 center(const sfrt_sphere& s) { return {s.x, s.y, s.z}; }
+
+bool finite3(const float* v) { return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]); }
+bool sphere_ok(const sfrt_sphere& s) {
+  return std::isfinite(s.x) && std::isfinite(s.y) && std::isfinite(s.z) && std::isfinite(s.radius) &&
+         s.radius > 0.0f;
+}
+
+// Stable insertion by |c - cam| + r, inserted after equal keys (SphereWorld.cpp:201-212).
+void sort_spheres(std::vector<sfrt_sphere>& spheres, V3 cam) {
+  std::vector<sfrt_sphere> temp = spheres;
+  spheres.clear();
+  for (const sfrt_sphere& t : temp) {
+    const float dist = vlength(vsub(center(t), cam)) + t.radius;
+    size_t ins = 0;
+    for (size_t j = 0; j < spheres.size(); j++) {
+      if (dist < vlength(vsub(center(spheres[j]), cam)) + spheres[j].radius) break;
+      ins++;
+    }
+    spheres.insert(spheres.begin() + (long)ins, t);
+  }
+}
+
+bool passes(float r, float s) { return r - std::sqrt(s) > 0.01f; }  // SphereWorld.cpp:365-366
+
+// Smallest binary32 s >= 0 for which the reference test fails; the test is
+// monotone in s (sqrtf and the subtraction are monotone), so
+// passes(r, s) <=> s < threshold for every s >= 0 (and NaN s fails both).
+float pass_threshold(float r) {
+  if (!passes(r, 0.0f)) return 0.0f;
+  uint32_t lo = 0, hi = 0x7f800000u;  // passes(lo), !passes(hi = +inf)
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    float s;
+    std::memcpy(&s, &mid, 4);
+    if (passes(r, s)) lo = mid; else hi = mid;
+  }
+  float t;
+  std::memcpy(&t, &hi, 4);
+  return t;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+#define HIP_TRY(expr)                          \
+  do {                                         \
+    if ((expr) != hipSuccess) return SFRT_E_HIP; \
+  } while (0)
+
+}  // namespace
+
+struct sfrt_world {
+  int device = 0;
+  // --- SphereWorld state read by UpdateImage ---
+  int width = 320;   // SphereWorld.h:50
+  int height = 180;  // SphereWorld.h:51
+  sfrt_camera cam{};
+  std::vector<sfrt_sphere> spheres;
+  std::vector<uint8_t> tex_host[SFRT_TEXTURE_SLOTS];
+  int tex_w[SFRT_TEXTURE_SLOTS] = {};
+  int tex_h[SFRT_TEXTURE_SLOTS] = {};
+  int cull = 1;
+  // --- device resources ---
+  hipStream_t stream = nullptr;
+  uint32_t* d_tex = nullptr;  // textures[0] on the device
+  size_t d_tex_texels = 0;
+  int* d_status = nullptr;
+  static constexpr int kRing = 8;
+  sfrt::SphereRec* d_spheres[kRing] = {};
+  int d_spheres_cap = 0;
+  int ring = 0;
+  uint32_t* d_frame = nullptr;  // compact subset buffer for the host path
+  size_t d_frame_px = 0;
+  uint32_t* h_stage = nullptr;  // pinned D2H staging
+  size_t h_stage_px = 0;
+  std::mutex mu;
+
+  ~sfrt_world() {
+    DeviceGuard g(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    (void)hipFree(d_tex);
+    (void)hipFree(d_status);
+    for (auto* p : d_spheres) (void)hipFree(p);
+    (void)hipFree(d_frame);
+    (void)hipHostFree(h_stage);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  int validate() const {
+    if (spheres.empty()) return SFRT_E_EMPTY;
+    if ((int)spheres.size() > SFRT_MAX_SPHERES) return SFRT_E_TOO_MANY;
+    if (tex_host[0].empty() || !d_tex) return SFRT_E_NO_TEXTURE;
+    if (width <= 0 || height <= 0) return SFRT_E_INVALID;
+    return SFRT_OK;
+  }
+
+  // Per-frame records: everything uniform over the frame, computed with the
+  // reference's expressions (see sfrt_trace.h).
+  void prepare(sfrt::FrameRec& f, std::vector<sfrt::SphereRec>& recs) const {
+    std::memset(&f, 0, sizeof f);
+    const V3 campos{cam.pos[0], cam.pos[1], cam.pos[2]};
+    f.cam[0] = campos.x; f.cam[1] = campos.y; f.cam[2] = campos.z;
+    // SphereWorld.cpp:100-104
+    V3 up = rot_x({0, -1, 0}, -cam.hrotation);
+    V3 forward = rot_x({0, 0, 1}, -cam.hrotation);
+    const V3 right = rot_y({1, 0, 0}, cam.rotation);
+    forward = rot_y(forward, cam.rotation);
+    up = rot_y(up, cam.rotation);
+    f.fwd[0] = forward.x; f.fwd[1] = forward.y; f.fwd[2] = forward.z;
+    f.right[0] = right.x; f.right[1] = right.y; f.right[2] = right.z;
+    f.up[0] = up.x; f.up[1] = up.y; f.up[2] = up.z;
+    // SphereWorld.cpp:85-89
+    f.v_start = -cam.fov_v;
+    f.v_inc = cam.fov_v / height * 2;
+    f.h_start = -cam.fov_h;
+    f.h_inc = cam.fov_h / width * 2;
+    // First march iteration (pos == cam.pos for every pixel), SphereWorld.cpp:362-370.
+    float largest = 0.0f;
+    int draw = 0;
+    for (size_t i = 0; i < spheres.size(); i++) {
+      const float dist = vlength(vsub(campos, center(spheres[i])));
+      if (spheres[i].radius - dist > 0.01f) {
+        const float t = spheres[i].radius - dist;
+        largest = largest < t ? t : largest;
+        draw = (int)i;
+      }
+    }
+    f.first_l = largest;
+    f.first_draw = draw;
+    f.n = (int)spheres.size();
+    f.width = width;
+    f.height = height;
+    f.tex_w = tex_w[0];
+    f.tex_h = tex_h[0];
+    f.tex_wf = (float)(unsigned)tex_w[0];
+    f.tex_hf = (float)(unsigned)tex_h[0];
+    f.cull = cull;
+    f.tex = d_tex;
+    f.status = d_status;
+    recs.resize(spheres.size());
+    for (size_t i = 0; i < spheres.size(); i++) {
+      const sfrt_sphere& s = spheres[i];
+      sfrt::SphereRec& r = recs[i];
+      r.cx = s.x; r.cy = s.y; r.cz = s.z; r.r = s.radius;
+      r.s_pass = pass_threshold(s.radius);
+      r.atan_c = sfrt_math::atan2f(s.z, s.x);  // == libm atan2f (tests/test_math_exhaustive.py)
+      r.pad0 = r.pad1 = 0.0f;
+    }
+  }
+
+  int ensure_sphere_buffers(int n) {
+    if (n <= d_spheres_cap) return SFRT_OK;
+    for (auto*& p : d_spheres) {
+      (void)hipFree(p);
+      p = nullptr;
+      HIP_TRY(hipMalloc(&p, sizeof(sfrt::SphereRec) * (size_t)n));
+    }
+    d_spheres_cap = n;
+    return SFRT_OK;
+  }
+
+  // Upload sphere records when the kernel reads them from device memory.
+  int stage_spheres(sfrt::FrameRec& f, const std::vector<sfrt::SphereRec>& recs, hipStream_t s,
+                    bool force) {
+    if (!force && f.n <= sfrt::kInlineSpheres) {
+      f.spheres = nullptr;
+      return SFRT_OK;
+    }
+    int rc = ensure_sphere_buffers(f.n);
+    if (rc) return rc;
+    sfrt::SphereRec* dst = d_spheres[ring];
+    ring = (ring + 1) % kRing;
+    // pageable source: the runtime stages it before returning, so recs may die after this.
+    HIP_TRY(hipMemcpyAsync(dst, recs.data(), sizeof(sfrt::SphereRec) * recs.size(),
+                           hipMemcpyHostToDevice, s));
+    f.spheres = dst;
+    return SFRT_OK;
+  }
+
+  int read_status(hipStream_t s) {
+    HIP_TRY(hipStreamSynchronize(s));
+    int st = 0;
+    HIP_TRY(hipMemcpy(&st, d_status, sizeof(int), hipMemcpyDeviceToHost));
+    if (st) HIP_TRY(hipMemset(d_status, 0, sizeof(int)));
+    if (st & 1) return SFRT_E_MARCH_LIMIT;
+    if (st & 2) return SFRT_E_TEXEL;
+    return SFRT_OK;
+  }
+};
+
+extern "C" {
+
+int sfrt_world_create(int hip_device, sfrt_world** out) {
+  if (!out) return SFRT_E_INVALID;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || hip_device < 0 || hip_device >= count)
+    return SFRT_E_HIP;
+  sfrt_world* w = new sfrt_world();
+  w->device = hip_device;
+  // Camera defaults (SphereWorld.h:10-21) and the constructor's conversion (:72-73).
+  w->cam.fov_h = sfrt_deg_to_rad(75.0f);
+  w->cam.fov_v = sfrt_deg_to_rad(47.0f);
+  DeviceGuard g(hip_device);
+  if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&w->d_status, sizeof(int)) != hipSuccess ||
+      hipMemset(w->d_status, 0, sizeof(int)) != hipSuccess) {
+    delete w;
+    return SFRT_E_HIP;
+  }
+  *out = w;
+  return SFRT_OK;
+}
+
+void sfrt_world_destroy(sfrt_world* w) { delete w; }
+
+int sfrt_world_set_size(sfrt_world* w, int width, int height) {
+  if (!w || width <= 0 || height <= 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  w->width = width;
+  w->height = height;
+  return SFRT_OK;
+}
+
+int sfrt_world_get_size(const sfrt_world* w, int* width, int* height) {
+  if (!w || !width || !height) return SFRT_E_INVALID;
+  *width = w->width;
+  *height = w->height;
+  return SFRT_OK;
+}
+
+int sfrt_world_set_camera(sfrt_world* w, const sfrt_camera* cam) {
+  if (!w || !cam || !finite3(cam->pos) || !std::isfinite(cam->rotation) ||
+      !std::isfinite(cam->hrotation) || !std::isfinite(cam->fov_h) || !std::isfinite(cam->fov_v))
+    return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  w->cam = *cam;
+  return SFRT_OK;
+}
+
+int sfrt_world_get_camera(const sfrt_world* w, sfrt_camera* cam) {
+  if (!w || !cam) return SFRT_E_INVALID;
+  *cam = w->cam;
+  return SFRT_OK;
+}
+
+int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int tex_w, int tex_h) {
+  if (!w || !rgba || slot < 0 || slot >= SFRT_TEXTURE_SLOTS || tex_w <= 0 || tex_h <= 0 ||
+      (int64_t)tex_w * tex_h > (1 << 28))
+    return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  const size_t bytes = (size_t)tex_w * tex_h * 4;
+  w->tex_host[slot].assign(rgba, rgba + bytes);
+  w->tex_w[slot] = tex_w;
+  w->tex_h[slot] = tex_h;
+  if (slot != 0) return SFRT_OK;  // only textures[0] is sampled (SphereWorld.cpp:376-377)
+  DeviceGuard g(w->device);
+  HIP_TRY(hipStreamSynchronize(w->stream));
+  if (w->d_tex_texels < (size_t)tex_w * tex_h) {
+    (void)hipFree(w->d_tex);
+    w->d_tex = nullptr;
+    HIP_TRY(hipMalloc(&w->d_tex, bytes));
+    w->d_tex_texels = (size_t)tex_w * tex_h;
+  }
+  HIP_TRY(hipMemcpy(w->d_tex, rgba, bytes, hipMemcpyHostToDevice));
+  return SFRT_OK;
+}
+
+int sfrt_world_add_sphere(sfrt_world* w, float x, float y, float z, float radius) {
+  const sfrt_sphere add{x, y, z, radius};
+  if (!w || !sphere_ok(add)) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  std::vector<sfrt_sphere>& s = w->spheres;
+  s.push_back(add);
+  // SphereWorld.cpp:180-188: drop every sphere contained in another one.
+  for (int i = 0; i < (int)s.size(); i++) {
+    for (int j = 0; j < (int)s.size(); j++) {
+      if (i != j && vlength(vsub(center(s[i]), center(s[j]))) + s[i].radius <= s[j].radius) {
+        s.erase(s.begin() + i);
+        i--;
+        break;
+      }
+    }
+  }
+  sort_spheres(s, {w->cam.pos[0], w->cam.pos[1], w->cam.pos[2]});
+  if ((int)s.size() > SFRT_MAX_SPHERES) return SFRT_E_TOO_MANY;
+  return SFRT_OK;
+}
+
+int sfrt_world_set_spheres(sfrt_world* w, const sfrt_sphere* spheres, int count) {
+  if (!w || count < 0 || (count > 0 && !spheres)) return SFRT_E_INVALID;
+  if (count > SFRT_MAX_SPHERES) return SFRT_E_TOO_MANY;
+  for (int i = 0; i < count; i++)
+    if (!sphere_ok(spheres[i])) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  w->spheres.assign(spheres, spheres + count);
+  return SFRT_OK;
+}
+
+int sfrt_world_get_spheres(const sfrt_world* w, sfrt_sphere* out, int capacity, int* count) {
+  if (!w || !count) return SFRT_E_INVALID;
+  *count = (int)w->spheres.size();
+  if (out) {
+    const int n = capacity < *count ? capacity : *count;
+    std::memcpy(out, w->spheres.data(), sizeof(sfrt_sphere) * (size_t)(n > 0 ? n : 0));
+  }
+  return SFRT_OK;
+}
+
+int sfrt_world_update_spheres(sfrt_world* w) {
+  if (!w) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  sort_spheres(w->spheres, {w->cam.pos[0], w->cam.pos[1], w->cam.pos[2]});
+  return SFRT_OK;
+}
+
+int sfrt_world_set_option(sfrt_world* w, int option, int value) {
+  if (!w) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  if (option == SFRT_OPT_CULL) {
+    w->cull = value ? 1 : 0;
+    return SFRT_OK;
+  }
+  return SFRT_E_INVALID;
+}
+
+int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart, int yadd, int xstart,
+                            int xadd) {
+  if (!w || !pixels || ystart < 0 || xstart < 0 || yadd <= 0 || xadd <= 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  int rc = w->validate();
+  if (rc) return rc;
+  // SphereWorld.cpp:94,97: i = xstart, xstart + xadd, ... < width (same for j).
+  const int sub_w = xstart < w->width ? (w->width - xstart + xadd - 1) / xadd : 0;
+  const int sub_h = ystart < w->height ? (w->height - ystart + yadd - 1) / yadd : 0;
+  if (sub_w == 0 || sub_h == 0) return SFRT_OK;
+  DeviceGuard g(w->device);
+  const size_t px = (size_t)sub_w * sub_h;
+  if (w->d_frame_px < px) {
+    (void)hipFree(w->d_frame);
+    w->d_frame = nullptr;
+    HIP_TRY(hipMalloc(&w->d_frame, px * 4));
+    w->d_frame_px = px;
+  }
+  if (w->h_stage_px < px) {
+    (void)hipHostFree(w->h_stage);
+    w->h_stage = nullptr;
+    HIP_TRY(hipHostMalloc(&w->h_stage, px * 4, hipHostMallocDefault));
+    w->h_stage_px = px;
+  }
+  sfrt::FrameRec f;
+  std::vector<sfrt::SphereRec> recs;
+  w->prepare(f, recs);
+  f.xstart = xstart; f.xadd = xadd; f.ystart = ystart; f.yadd = yadd;
+  f.sub_w = sub_w;
+  f.sub_row0 = 0;
+  f.sub_rows = sub_h;
+  f.tiles_x = (sub_w + sfrt::kTile - 1) / sfrt::kTile;
+  f.out = w->d_frame;
+  f.out_pitch = sub_w;
+  rc = w->stage_spheres(f, recs, w->stream, false);
+  if (rc) return rc;
+  if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
+  HIP_TRY(hipMemcpyAsync(w->h_stage, w->d_frame, px * 4, hipMemcpyDeviceToHost, w->stream));
+  rc = w->read_status(w->stream);
+  if (rc) return rc;
+  // Scatter the subset into the caller's frame: only addressed pixels are written.
+  const size_t W = (size_t)w->width;
+  for (int bb = 0; bb < sub_h; bb++) {
+    const size_t j = (size_t)ystart + (size_t)bb * yadd;
+    const uint32_t* src = w->h_stage + (size_t)bb * sub_w;
+    uint8_t* row = pixels + j * W * 4;
+    if (xadd == 1) {
+      std::memcpy(row + (size_t)xstart * 4, src, (size_t)sub_w * 4);
+    } else {
+      for (int a = 0; a < sub_w; a++)
+        std::memcpy(row + ((size_t)xstart + (size_t)a * xadd) * 4, src + a, 4);
+    }
+  }
+  return SFRT_OK;
+}
+
+int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes, int row0,
+                           int rows, void* hip_stream) {
+  if (!w || !dev_pixels || row0 < 0 || rows < 0 || pitch_bytes % 4 != 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  int rc = w->validate();
+  if (rc) return rc;
+  if (pitch_bytes < (int64_t)w->width * 4 || row0 + rows > w->height) return SFRT_E_INVALID;
+  if (rows == 0) return SFRT_OK;
+  DeviceGuard g(w->device);
+  hipStream_t s = (hipStream_t)hip_stream;  // HIP convention: NULL = the null stream
+  sfrt::FrameRec f;
+  std::vector<sfrt::SphereRec> recs;
+  w->prepare(f, recs);
+  f.xstart = 0; f.xadd = 1; f.ystart = 0; f.yadd = 1;
+  f.sub_w = w->width;
+  f.sub_row0 = row0;
+  f.sub_rows = rows;
+  f.tiles_x = (w->width + sfrt::kTile - 1) / sfrt::kTile;
+  f.out = (uint32_t*)dev_pixels;
+  f.out_pitch = pitch_bytes / 4;
+  rc = w->stage_spheres(f, recs, s, false);
+  if (rc) return rc;
+  return sfrt::launch_trace(f, recs.data(), s) ? SFRT_E_HIP : SFRT_OK;
+}
+
+int sfrt_world_check(sfrt_world* w, void* hip_stream) {
+  if (!w) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  DeviceGuard g(w->device);
+  return w->read_status((hipStream_t)hip_stream);
+}
+
+int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pixel_dump* out) {
+  if (!w || count < 0 || (count > 0 && (!ij || !out))) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  int rc = w->validate();
+  if (rc) return rc;
+  for (int k = 0; k < count; k++)
+    if (ij[2 * k] < 0 || ij[2 * k] >= w->width || ij[2 * k + 1] < 0 || ij[2 * k + 1] >= w->height)
+      return SFRT_E_INVALID;
+  if (count == 0) return SFRT_OK;
+  static_assert(sizeof(sfrt_pixel_dump) == sizeof(sfrt::PixelDump), "dump layout");
+  DeviceGuard g(w->device);
+  sfrt::FrameRec f;
+  std::vector<sfrt::SphereRec> recs;
+  w->prepare(f, recs);
+  rc = w->stage_spheres(f, recs, w->stream, true);
+  if (rc) return rc;
+  int32_t* d_ij = nullptr;
+  sfrt::PixelDump* d_out = nullptr;
+  if (hipMalloc(&d_ij, sizeof(int32_t) * 2 * (size_t)count) != hipSuccess ||
+      hipMalloc(&d_out, sizeof(sfrt::PixelDump) * (size_t)count) != hipSuccess) {
+    (void)hipFree(d_ij);
+    return SFRT_E_HIP;
+  }
+  rc = SFRT_OK;
+  if (hipMemcpyAsync(d_ij, ij, sizeof(int32_t) * 2 * (size_t)count, hipMemcpyHostToDevice,
+                     w->stream) != hipSuccess ||
+      sfrt::launch_trace_points(f, d_ij, count, d_out, w->stream) ||
+      hipMemcpyAsync(out, d_out, sizeof(sfrt::PixelDump) * (size_t)count, hipMemcpyDeviceToHost,
+                     w->stream) != hipSuccess)
+    rc = SFRT_E_HIP;
+  const int st = w->read_status(w->stream);
+  (void)hipFree(d_ij);
+  (void)hipFree(d_out);
+  return rc ? rc : st;
+}
+
+int sfrt_sort_spheres(sfrt_sphere* spheres, int count, const float cam_pos[3]) {
+  if (count < 0 || (count > 0 && !spheres) || !cam_pos) return SFRT_E_INVALID;
+  std::vector<sfrt_sphere> v(spheres, spheres + count);
+  sort_spheres(v, {cam_pos[0], cam_pos[1], cam_pos[2]});
+  std::memcpy(spheres, v.data(), sizeof(sfrt_sphere) * (size_t)count);
+  return SFRT_OK;
+}
+
+float sfrt_deg_to_rad(float deg) { return deg * (kPI / 180.0f); }
+
+float sfrt_pass_threshold(float radius) { return pass_threshold(radius); }
+
+const char* sfrt_error_string(int code) {
+  switch (code) {
+    case SFRT_OK: return "ok";
+    case SFRT_E_INVALID: return "invalid argument";
+    case SFRT_E_EMPTY: return "no spheres (reference: std::out_of_range from spheres.at)";
+    case SFRT_E_NO_TEXTURE: return "texture slot 0 not loaded";
+    case SFRT_E_TOO_MANY: return "too many spheres";
+    case SFRT_E_HIP: return "HIP runtime error";
+    case SFRT_E_MARCH_LIMIT: return "march iteration limit exceeded";
+    case SFRT_E_TEXEL: return "texel index outside the texture";
+    default: return "unknown error";
+  }
+}
+
+int sfrt_version(void) { return 1; }
+
+}  // extern "C"

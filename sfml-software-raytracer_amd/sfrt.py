@@ -1,0 +1,265 @@
+"""Python plumbing over libsfrt.so (the C ABI in include/sfrt.h).
+
+Used by bench.py, __graft_entry__.py and the tests.  The class ``World``
+mirrors the reference's ``SphereWorld`` surface for this path
+(/root/reference/Raytracing/SphereWorld.h:40-78): ``width``/``height``,
+``cam``, ``AddSphere``, ``UpdateSpheres`` and ``UpdateImage(ystart, yadd,
+xstart, xadd)``, plus the device-resident ``render_band`` used by the display
+and multi-GPU paths.  There is no CPU fallback: if libsfrt.so is missing or
+has no HIP device, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsfrt.so")
+
+SFRT_OPT_CULL = 1
+ERRORS = {
+    0: "SFRT_OK", -1: "SFRT_E_INVALID", -2: "SFRT_E_EMPTY", -3: "SFRT_E_NO_TEXTURE",
+    -4: "SFRT_E_TOO_MANY", -5: "SFRT_E_HIP", -6: "SFRT_E_MARCH_LIMIT", -7: "SFRT_E_TEXEL",
+}
+
+# Every symbol include/sfrt.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = (
+    "sfrt_world_create", "sfrt_world_destroy", "sfrt_world_set_size", "sfrt_world_get_size",
+    "sfrt_world_set_camera", "sfrt_world_get_camera", "sfrt_world_load_texture",
+    "sfrt_world_add_sphere", "sfrt_world_set_spheres", "sfrt_world_get_spheres",
+    "sfrt_world_update_spheres", "sfrt_world_update_image", "sfrt_world_render_band",
+    "sfrt_world_check", "sfrt_world_trace_points", "sfrt_world_set_option",
+    "sfrt_sort_spheres", "sfrt_deg_to_rad", "sfrt_pass_threshold", "sfrt_error_string",
+    "sfrt_version",
+)
+
+
+class SfrtError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        super().__init__(f"{what}: {ERRORS.get(code, code)} ({code})")
+
+
+class Sphere(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("z", ctypes.c_float),
+                ("radius", ctypes.c_float)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_float * 3), ("rotation", ctypes.c_float),
+                ("hrotation", ctypes.c_float), ("fov_h", ctypes.c_float),
+                ("fov_v", ctypes.c_float)]
+
+
+class PixelDump(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_float * 3), ("draw", ctypes.c_int32), ("iters", ctypes.c_int32),
+                ("xcoord", ctypes.c_float), ("ycoord", ctypes.c_float),
+                ("brightness", ctypes.c_float), ("texel", ctypes.c_uint32 * 2),
+                ("rgba", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsfrt.so (raises if it was not built: no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build() (make -C "
+                           f"sfml-software-raytracer_amd)")
+    # torch wheels bundle their own libamdhip64 (same soname).  Loading torch first
+    # lets libsfrt.so bind to that one, so a process has ONE HIP runtime and torch
+    # tensors / streams can be handed to render_band.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    P, c_int, c_float, vp = ctypes.POINTER, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
+    W = vp  # opaque sfrt_world*
+    sig = {
+        "sfrt_world_create": ([c_int, P(vp)], c_int),
+        "sfrt_world_destroy": ([W], None),
+        "sfrt_world_set_size": ([W, c_int, c_int], c_int),
+        "sfrt_world_get_size": ([W, P(c_int), P(c_int)], c_int),
+        "sfrt_world_set_camera": ([W, P(Camera)], c_int),
+        "sfrt_world_get_camera": ([W, P(Camera)], c_int),
+        "sfrt_world_load_texture": ([W, c_int, vp, c_int, c_int], c_int),
+        "sfrt_world_add_sphere": ([W, c_float, c_float, c_float, c_float], c_int),
+        "sfrt_world_set_spheres": ([W, vp, c_int], c_int),
+        "sfrt_world_get_spheres": ([W, vp, c_int, P(c_int)], c_int),
+        "sfrt_world_update_spheres": ([W], c_int),
+        "sfrt_world_update_image": ([W, vp, c_int, c_int, c_int, c_int], c_int),
+        "sfrt_world_render_band": ([W, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
+        "sfrt_world_check": ([W, vp], c_int),
+        "sfrt_world_trace_points": ([W, vp, c_int, vp], c_int),
+        "sfrt_world_set_option": ([W, c_int, c_int], c_int),
+        "sfrt_sort_spheres": ([vp, c_int, vp], c_int),
+        "sfrt_deg_to_rad": ([c_float], c_float),
+        "sfrt_pass_threshold": ([c_float], c_float),
+        "sfrt_error_string": ([c_int], ctypes.c_char_p),
+        "sfrt_version": ([], c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise SfrtError(rc, what)
+
+
+def _f32_rows(spheres) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(spheres, dtype=np.float32).reshape(-1, 4))
+
+
+def sort_spheres(spheres, cam_pos=(0.0, 0.0, 0.0)) -> np.ndarray:
+    s = _f32_rows(spheres).copy()
+    cam = (ctypes.c_float * 3)(*[float(c) for c in cam_pos])
+    _check(lib().sfrt_sort_spheres(s.ctypes.data, s.shape[0], cam), "sfrt_sort_spheres")
+    return s
+
+
+def deg_to_rad(deg: float) -> float:
+    return lib().sfrt_deg_to_rad(float(deg))
+
+
+def pass_threshold(radius: float) -> float:
+    return lib().sfrt_pass_threshold(float(radius))
+
+
+class World:
+    """Device-backed mirror of ``SphereWorld`` for the frame-fill path."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().sfrt_world_create(int(device), ctypes.byref(h)), "sfrt_world_create")
+        self._h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().sfrt_world_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # --- state ---
+    def set_size(self, width: int, height: int) -> None:
+        _check(lib().sfrt_world_set_size(self._h, int(width), int(height)), "set_size")
+
+    @property
+    def size(self) -> tuple[int, int]:
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sfrt_world_get_size(self._h, ctypes.byref(w), ctypes.byref(h)), "get_size")
+        return w.value, h.value
+
+    def set_camera(self, pos=(0.0, 0.0, 0.0), rotation=0.0, hrotation=0.0, fov_h=None,
+                   fov_v=None) -> None:
+        cur = self.camera
+        cam = Camera()
+        for k in range(3):
+            cam.pos[k] = float(pos[k])
+        cam.rotation, cam.hrotation = float(rotation), float(hrotation)
+        cam.fov_h = float(fov_h) if fov_h is not None else cur.fov_h
+        cam.fov_v = float(fov_v) if fov_v is not None else cur.fov_v
+        _check(lib().sfrt_world_set_camera(self._h, ctypes.byref(cam)), "set_camera")
+
+    @property
+    def camera(self) -> Camera:
+        cam = Camera()
+        _check(lib().sfrt_world_get_camera(self._h, ctypes.byref(cam)), "get_camera")
+        return cam
+
+    def load_texture(self, rgba, tex_w: int, tex_h: int, slot: int = 0) -> None:
+        buf = np.ascontiguousarray(np.asarray(rgba, dtype=np.uint8).ravel())
+        if buf.size != tex_w * tex_h * 4:
+            raise ValueError("texture size mismatch")
+        _check(lib().sfrt_world_load_texture(self._h, slot, buf.ctypes.data, tex_w, tex_h),
+               "load_texture")
+
+    def add_sphere(self, x, y, z, radius) -> None:
+        _check(lib().sfrt_world_add_sphere(self._h, float(x), float(y), float(z), float(radius)),
+               "add_sphere")
+
+    def set_spheres(self, spheres) -> None:
+        s = _f32_rows(spheres)
+        _check(lib().sfrt_world_set_spheres(self._h, s.ctypes.data, s.shape[0]), "set_spheres")
+
+    @property
+    def spheres(self) -> np.ndarray:
+        n = ctypes.c_int()
+        _check(lib().sfrt_world_get_spheres(self._h, None, 0, ctypes.byref(n)), "get_spheres")
+        out = np.zeros((n.value, 4), dtype=np.float32)
+        _check(lib().sfrt_world_get_spheres(self._h, out.ctypes.data, n.value, ctypes.byref(n)),
+               "get_spheres")
+        return out
+
+    def update_spheres(self) -> None:
+        _check(lib().sfrt_world_update_spheres(self._h), "update_spheres")
+
+    def set_option(self, option: int, value: int) -> None:
+        _check(lib().sfrt_world_set_option(self._h, option, value), "set_option")
+
+    def set_scene(self, scene, width: int, height: int) -> None:
+        """Load a scenes.Scene (spheres verbatim, camera pose) at width x height."""
+        self.set_size(width, height)
+        self.set_camera(scene.cam_pos, scene.rotation, scene.hrotation, scene.fov_h, scene.fov_v)
+        self.set_spheres(scene.spheres)
+
+    # --- frame fill ---
+    def update_image(self, pixels: np.ndarray, ystart=0, yadd=1, xstart=0, xadd=1) -> np.ndarray:
+        """SphereWorld::UpdateImage into a host RGBA8 buffer (width*height*4 bytes)."""
+        w, h = self.size
+        if pixels.dtype != np.uint8 or pixels.size != w * h * 4 or not pixels.flags.c_contiguous:
+            raise ValueError("pixels must be a contiguous uint8 array of width*height*4")
+        _check(lib().sfrt_world_update_image(self._h, pixels.ctypes.data, ystart, yadd, xstart,
+                                             xadd), "update_image")
+        return pixels
+
+    def render(self) -> np.ndarray:
+        w, h = self.size
+        out = np.zeros(w * h * 4, dtype=np.uint8)
+        return self.update_image(out)
+
+    def render_band(self, dev_ptr: int, pitch_bytes: int, row0: int, rows: int,
+                    stream: int = 0) -> None:
+        """Asynchronous device fill of rows [row0, row0+rows) at dev_ptr on `stream`."""
+        _check(lib().sfrt_world_render_band(self._h, ctypes.c_void_p(dev_ptr), int(pitch_bytes),
+                                            int(row0), int(rows), ctypes.c_void_p(stream or None)),
+               "render_band")
+
+    def check(self, stream: int = 0) -> None:
+        _check(lib().sfrt_world_check(self._h, ctypes.c_void_p(stream or None)), "check")
+
+    def trace_points(self, ij) -> list[dict]:
+        ij = np.ascontiguousarray(np.asarray(ij, dtype=np.int32).reshape(-1, 2))
+        out = (PixelDump * ij.shape[0])()
+        _check(lib().sfrt_world_trace_points(self._h, ij.ctypes.data, ij.shape[0],
+                                             ctypes.cast(out, ctypes.c_void_p)), "trace_points")
+        res = []
+        for d in out:
+            rgba = d.rgba
+            res.append({"pos": list(d.pos), "draw": d.draw, "iters": d.iters,
+                        "xcoord": d.xcoord, "ycoord": d.ycoord, "brightness": d.brightness,
+                        "texel": list(d.texel),
+                        "rgba": [rgba & 255, (rgba >> 8) & 255, (rgba >> 16) & 255, rgba >> 24]})
+        return res

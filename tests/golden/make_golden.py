@@ -1,0 +1,79 @@
+"""Generate tests/golden/ from the CPU restatement (oracle/).
+
+    python tests/golden/make_golden.py
+
+Writes golden.json: per (config, pose) the frame's FNV-1a-64 and SHA-256,
+per-row FNV-1a-64 for frames up to 4K, the march-iteration statistics, and
+~1000 sampled-pixel float dumps for two configs; plus the full 320x240 frame
+(zlib-compressed RGBA8).  The oracle's iteration statistics are pinned to the
+survey's probe of the unmodified reference by
+tests/test_oracle_golden.py; see DESIGN.md "Parity pinning".
+"""
+import hashlib
+import json
+import os
+import platform
+import sys
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle  # noqa: E402
+import scenes  # noqa: E402
+
+DUMP_CONFIGS = {("c2_1920x1080_default10", (0.7, 0.3)), ("c3_3840x2160_lcg64", (0.0, 0.0))}
+
+
+def row_hashes(frame, width, height):
+    rows = frame.reshape(height, width * 4)
+    return [oracle.fnv1a64(rows[j]) for j in range(height)]
+
+
+def iteration_stats(o, width, height):
+    it = o.iteration_map(os.cpu_count() or 1)
+    return {"mean": round(float(it.mean()), 4), "p99": int(np.percentile(it, 99)),
+            "max": int(it.max())}
+
+
+def main():
+    oracle.build()
+    tex, tw, th = scenes.load_floor()
+    threads = os.cpu_count() or 1
+    out = {"generator": "tests/golden/make_golden.py (oracle/sphereworld_oracle.c)",
+           "libc": " ".join(platform.libc_ver()), "texture_sha256":
+           hashlib.sha256(tex.tobytes()).hexdigest(), "frames": {}, "dumps": {}}
+    for cfg, (width, height, sname, poses) in scenes.CONFIGS.items():
+        for pose in poses:
+            key = f"{cfg}@{pose[0]:g},{pose[1]:g}"
+            scene = scenes.SCENES[sname]().posed(*pose)
+            o = oracle.Oracle.from_scene(scene, width, height, tex, tw, th)
+            frame = o.render(threads)
+            ent = {"config": cfg, "scene": sname, "pose": list(pose), "width": width,
+                   "height": height, "fnv1a64": oracle.fnv1a64(frame),
+                   "sha256": hashlib.sha256(frame.tobytes()).hexdigest()}
+            if width * height <= 3840 * 2160:
+                ent["row_fnv1a64"] = row_hashes(frame, width, height)
+                ent["iterations"] = iteration_stats(o, width, height)
+            if width * height <= 320 * 240:
+                fn = f"frame_{cfg}.rgba.zlib"
+                with open(os.path.join(HERE, fn), "wb") as f:
+                    f.write(zlib.compress(frame.tobytes(), 9))
+                ent["frame_file"] = fn
+            out["frames"][key] = ent
+            if (cfg, pose) in DUMP_CONFIGS:
+                rng = np.random.default_rng(99)
+                ij = np.stack([rng.integers(0, width, 1000), rng.integers(0, height, 1000)], 1)
+                out["dumps"][key] = [dict(o.dump(int(i), int(j)), i=int(i), j=int(j))
+                                     for i, j in ij]
+            print(key, ent["fnv1a64"], flush=True)
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,124 @@
+// Device check of sfrt_math.h on gfx950 against the host libm (glibc 2.35).
+// Built and run by tests/test_gpu_parity.py::test_device_math_matches_libm:
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fopenmp math_gpu_check.hip
+//   ./math_gpu_check asinf|atanf [stride]   -> every stride-th binary32 pattern
+//   ./math_gpu_check atan2f <npairs>        -> random + scene-range pairs
+//   ./math_gpu_check sqrt_div [stride]      -> correctly rounded sqrtf and x/y vs the host
+// Prints "<fn> checked=<n> mismatches=<m>".
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../sfml-software-raytracer_amd/csrc/sfrt_math.h"
+
+#pragma clang fp contract(off)
+
+__global__ void k_eval(int fn, const float* __restrict__ x, const float* __restrict__ y,
+                       float* __restrict__ out, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float r;
+  switch (fn) {
+    case 0: r = sfrt_math::asinf(x[i]); break;
+    case 1: r = sfrt_math::atanf(x[i]); break;
+    case 2: r = sfrt_math::atan2f(x[i], y[i]); break;
+    case 3: r = __builtin_sqrtf(x[i]); break;
+    default: r = x[i] / y[i]; break;
+  }
+  out[i] = r;
+}
+
+static float host_eval(int fn, float x, float y) {
+  switch (fn) {
+    case 0: return ::asinf(x);
+    case 1: return ::atanf(x);
+    case 2: return ::atan2f(x, y);
+    case 3: return std::sqrt(x);
+    default: return x / y;
+  }
+}
+
+static inline uint32_t bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float fl(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+static uint64_t mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) return 2;
+  int fn;
+  if (!strcmp(argv[1], "asinf")) fn = 0;
+  else if (!strcmp(argv[1], "atanf")) fn = 1;
+  else if (!strcmp(argv[1], "atan2f")) fn = 2;
+  else if (!strcmp(argv[1], "sqrt_div")) fn = 3;
+  else return 2;
+  const long long total = fn == 2 ? (argc > 2 ? atoll(argv[2]) : 100000000LL)
+                                  : (4294967296LL / (argc > 2 ? atoll(argv[2]) : 1));
+  const long long stride = fn == 2 ? 1 : (argc > 2 ? atoll(argv[2]) : 1);
+  const long chunk = 1L << 26;
+  std::vector<float> hx(chunk), hy(chunk), hout(chunk);
+  float *dx, *dy, *dout;
+  if (hipMalloc(&dx, chunk * 4) || hipMalloc(&dy, chunk * 4) || hipMalloc(&dout, chunk * 4)) {
+    printf("hipMalloc failed\n");
+    return 3;
+  }
+  unsigned long long checked = 0, bad = 0;
+  const int passes = fn == 3 ? 2 : 1;  // sqrt_div: pass 0 sqrtf, pass 1 division
+  for (int pass = 0; pass < passes; pass++) {
+    const int f = fn == 3 ? 3 + pass : fn;
+    for (long long base = 0; base < total; base += chunk) {
+      const long n = (long)((total - base) < chunk ? (total - base) : chunk);
+#pragma omp parallel for schedule(static)
+      for (long i = 0; i < n; i++) {
+        const long long k = base + i;
+        if (f == 2 || f == 4) {
+          const uint64_t z = mix((uint64_t)k * 0x9E3779B97F4A7C15ULL + 7);
+          if (k & 1) {
+            hx[i] = fl((uint32_t)z);
+            hy[i] = fl((uint32_t)(z >> 32));
+          } else {
+            hx[i] = ((float)(uint32_t)z / 4294967296.0f - 0.5f) * 128.0f;
+            hy[i] = ((float)(uint32_t)(z >> 32) / 4294967296.0f - 0.5f) * 128.0f;
+          }
+        } else {
+          hx[i] = fl((uint32_t)(k * stride));
+          hy[i] = 0.0f;
+        }
+      }
+      if (hipMemcpy(dx, hx.data(), n * 4, hipMemcpyHostToDevice) ||
+          hipMemcpy(dy, hy.data(), n * 4, hipMemcpyHostToDevice))
+        return 3;
+      hipLaunchKernelGGL(k_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, f, dx, dy, dout, n);
+      if (hipMemcpy(hout.data(), dout, n * 4, hipMemcpyDeviceToHost)) return 3;
+      unsigned long long b = 0;
+#pragma omp parallel for reduction(+ : b) schedule(static)
+      for (long i = 0; i < n; i++) {
+        const float want = host_eval(f, hx[i], hy[i]);
+        const float got = hout[i];
+        const bool ok = (std::isnan(want) && std::isnan(got)) || bits(want) == bits(got);
+        if (!ok) b++;
+      }
+      if (b && bad < 1) {
+        for (long i = 0; i < n; i++) {
+          const float want = host_eval(f, hx[i], hy[i]);
+          if (!((std::isnan(want) && std::isnan(hout[i])) || bits(want) == bits(hout[i]))) {
+            printf("MISMATCH fn=%d x=%a y=%a host=%a gpu=%a\n", f, hx[i], hy[i], want, hout[i]);
+            break;
+          }
+        }
+      }
+      bad += b;
+      checked += n;
+    }
+  }
+  printf("%s checked=%llu mismatches=%llu\n", argv[1], checked, bad);
+  return bad ? 1 : 0;
+}

@@ -1,0 +1,112 @@
+"""The C-ABI library loads without a GPU, exports every symbol include/sfrt.h
+declares, and its host-side helpers agree with the restatement."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+import scenes
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def lib(built):
+    import sfrt
+    return sfrt.lib()
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "sfrt.h")).read()
+    return sorted(set(re.findall(r"^SFRT_API [^;]*?\b(sfrt_\w+)\s*\(", text, re.M)))
+
+
+def test_exports_every_declared_symbol(lib):
+    import sfrt
+    names = header_symbols()
+    assert len(names) >= 20
+    assert set(names) == set(sfrt.ABI_SYMBOLS)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_only_abi_symbols_are_exported():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only",
+                          os.path.join(ROOT, "sfml-software-raytracer_amd", "libsfrt.so")],
+                         capture_output=True, text=True, check=True).stdout
+    funcs = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert funcs == set(header_symbols())
+
+
+def test_world_create_without_gpu_fails_loudly(lib):
+    import sfrt
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    h = ctypes.c_void_p()
+    assert lib.sfrt_world_create(0, ctypes.byref(h)) == -5  # SFRT_E_HIP, no CPU fallback
+    with pytest.raises(sfrt.SfrtError):
+        sfrt.World(0)
+
+
+def test_error_strings(lib):
+    for code in range(0, -8, -1):
+        assert lib.sfrt_error_string(code)
+    assert lib.sfrt_version() >= 1
+
+
+def test_deg_to_rad_matches_reference_expression(lib):
+    for d in (75.0, 47.0, 90.0, 1.0, 123.456):
+        assert np.float32(lib.sfrt_deg_to_rad(d)) == scenes.deg2rad(d)
+        assert np.float32(lib.sfrt_deg_to_rad(d)) == np.float32(oracle.lib().oracle_deg2rad(d))
+
+
+def _passes(r, s):
+    r, s = np.float32(r), np.float32(s)
+    return bool(np.float32(r - np.sqrt(s)) > np.float32(0.01))
+
+
+def test_pass_threshold_is_exact(lib):
+    rng = np.random.default_rng(5)
+    radii = np.concatenate([np.arange(1, 9, dtype=np.float32),
+                            rng.uniform(0.005, 500, 300).astype(np.float32),
+                            np.float32([0.01, 0.0100001, 0.02, 1e-6, 3e7])])
+    for r in radii:
+        t = np.float32(lib.sfrt_pass_threshold(float(r)))
+        if t == 0:
+            assert not _passes(r, 0.0)
+            continue
+        below = np.nextafter(t, np.float32(0))
+        assert _passes(r, below) and not _passes(r, t), r
+        # spot-check monotonicity further away on both sides
+        for s in (t * np.float32(0.5), below * np.float32(0.999)):
+            assert _passes(r, s)
+        for s in (t * np.float32(1.001), t * np.float32(2)):
+            assert not _passes(r, s)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_sort_spheres_matches_update_spheres(lib, seed):
+    import sfrt
+    rng = np.random.default_rng(seed)
+    sp = np.concatenate([scenes.lcg_spheres(count=40, seed=seed),
+                         # exact key ties exercise the "insert after equal keys" rule
+                         np.float32([[3, 0, 0, 2], [0, 3, 0, 2], [0, 0, -3, 2], [3, 0, 0, 2]])])
+    rng.shuffle(sp)
+    cam = tuple(rng.uniform(-2, 2, 3).astype(np.float32))
+    a = sfrt.sort_spheres(sp, cam)
+    b = oracle.sort_spheres(sp, cam)
+    c = scenes.sort_spheres(sp, cam)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+def test_lcg64_scene_shape():
+    s = scenes.lcg64().spheres
+    assert s.shape == (64, 4)
+    assert (s[:, 3] >= 2).all() and (s[:, 3] <= 7).all()
+    # first draws of the MSVC LCG, seed 12345 (s = s*214013 + 2531011, r = (s >> 16) & 0x7fff)
+    st, r = scenes.msvc_rand(12345)
+    assert r == ((12345 * 214013 + 2531011) & 0xFFFFFFFF) >> 16 & 0x7FFF

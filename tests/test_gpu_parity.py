@@ -1,0 +1,205 @@
+"""GPU parity: libsfrt.so (HIP, gfx950) against the CPU restatement, byte for byte.
+
+Every frame here goes through the C ABI (sfrt.World -> libsfrt.so).  The
+oracle (oracle/, TEST INFRASTRUCTURE) renders the same scene on the host
+cores; frames too large for that in seconds are checked against the committed
+golden hashes in tests/golden/golden.json instead.  Bar: RGBA8 bit-exact;
+float intermediates (march position, xcoord, ycoord, brightness) within
+1e-5 absolute (they are in fact expected to be identical) and integer ones
+(drawSphere, iterations, texel) exact.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import scenes
+from conftest import ROOT, host_threads
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+FLOAT_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def world(built, floor):
+    import sfrt
+    w = sfrt.World(0)
+    w.load_texture(*floor)
+    yield w
+    w.close()
+
+
+def oracle_for(scene, width, height, floor):
+    import oracle
+    return oracle.Oracle.from_scene(scene, width, height, *floor)
+
+
+def diff_report(got, want, width):
+    g = got.reshape(-1, 4)
+    w = want.reshape(-1, 4)
+    bad = np.nonzero(np.any(g != w, axis=1))[0]
+    if bad.size == 0:
+        return ""
+    k = int(bad[0])
+    return (f"{bad.size} pixels differ; first at (i={k % width}, j={k // width}): "
+            f"gpu={g[k].tolist()} oracle={w[k].tolist()}")
+
+
+ORACLE_CASES = [
+    ("c1_320x240_one_sphere", (0.0, 0.0)),
+    ("c2_1920x1080_default10", (0.0, 0.0)),
+    ("c2_1920x1080_default10", (0.7, 0.3)),
+    ("c3_3840x2160_lcg64", (0.0, 0.0)),
+    ("c3_3840x2160_lcg64", (1.1, -0.2)),
+    ("c3_3840x2160_default10", (0.0, 0.0)),
+]
+
+
+@pytest.mark.parametrize("cfg,pose", ORACLE_CASES)
+def test_full_frame_matches_oracle(world, floor, cfg, pose):
+    width, height, sname, _ = scenes.CONFIGS[cfg]
+    scene = scenes.SCENES[sname]().posed(*pose)
+    world.set_scene(scene, width, height)
+    got = world.render()
+    want = oracle_for(scene, width, height, floor).render(host_threads())
+    msg = diff_report(got, want, width)
+    assert not msg, f"{cfg} pose={pose}: {msg}"
+
+
+@pytest.mark.parametrize("key", sorted(k for k in GOLDEN["frames"]
+                                       if GOLDEN["frames"][k]["width"] * GOLDEN["frames"][k]["height"] > 3840 * 2160))
+def test_large_frame_matches_golden_hash(world, key):
+    """8K and 16K^2 frames: device render, FNV-1a-64 vs the committed oracle hash."""
+    import oracle
+    g = GOLDEN["frames"][key]
+    scene = scenes.SCENES[g["scene"]]().posed(*g["pose"])
+    world.set_scene(scene, g["width"], g["height"])
+    got = world.render()
+    assert oracle.fnv1a64(got) == g["fnv1a64"], key
+
+
+def test_cull_on_off_identical(world, floor):
+    """Per-wave culling must not change a byte (A/B over the rotated 64-sphere 4K pose)."""
+    import sfrt
+    scene = scenes.lcg64().posed(1.1, -0.2)
+    world.set_scene(scene, 3840, 2160)
+    a = world.render()
+    world.set_option(sfrt.SFRT_OPT_CULL, 0)
+    try:
+        b = world.render()
+    finally:
+        world.set_option(sfrt.SFRT_OPT_CULL, 1)
+    assert diff_report(a, b, 3840) == ""
+
+
+@pytest.mark.parametrize("ystart,yadd,xstart,xadd", [
+    (0, 8, 0, 4), (3, 8, 2, 4), (7, 8, 3, 4),   # RenderThread interleave (Source.cpp:21,23)
+    (1, 3, 0, 1), (0, 1, 5, 7), (239, 1, 319, 1), (5, 1000, 0, 1)])
+def test_update_image_subset_writes_only_addressed(world, floor, ystart, yadd, xstart, xadd):
+    width, height = 320, 240
+    scene = scenes.default10().posed(0.7, 0.3)
+    world.set_scene(scene, width, height)
+    canvas = np.full(width * height * 4, 0xA5, dtype=np.uint8)
+    expect = canvas.copy()
+    world.update_image(canvas, ystart, yadd, xstart, xadd)
+    oracle_for(scene, width, height, floor).update_image(expect, ystart, yadd, xstart, xadd)
+    assert diff_report(canvas, expect, width) == ""
+
+
+def test_row_bands_tile_the_frame(world, floor):
+    """Multi-GPU row bands: bands rendered separately == the single-launch frame."""
+    import torch
+    width, height = 1920, 1080
+    scene = scenes.lcg64().posed(0.3, 0.1)
+    world.set_scene(scene, width, height)
+    full = torch.zeros(height, width * 4, dtype=torch.uint8, device="cuda:0")
+    bands = torch.zeros_like(full)
+    stream = torch.cuda.current_stream().cuda_stream
+    world.render_band(full.data_ptr(), width * 4, 0, height, stream)
+    for r0, r1 in [(0, 1), (1, 270), (270, 541), (541, 1079), (1079, 1080)]:
+        world.render_band(bands[r0].data_ptr(), width * 4, r0, r1 - r0, stream)
+    world.check(stream)
+    torch.cuda.synchronize()
+    f = full.cpu().numpy().ravel()
+    b = bands.cpu().numpy().ravel()
+    assert diff_report(b, f, width) == ""
+    want = oracle_for(scene, width, height, floor).render(host_threads())
+    assert diff_report(f, want, width) == ""
+
+
+@pytest.mark.parametrize("cfg,pose", [("c2_1920x1080_default10", (0.7, 0.3)),
+                                      ("c3_3840x2160_lcg64", (0.0, 0.0))])
+def test_float_intermediates(world, floor, cfg, pose):
+    width, height, sname, _ = scenes.CONFIGS[cfg]
+    scene = scenes.SCENES[sname]().posed(*pose)
+    world.set_scene(scene, width, height)
+    rng = np.random.default_rng(1234)
+    ij = np.stack([rng.integers(0, width, 1000), rng.integers(0, height, 1000)], axis=1)
+    got = world.trace_points(ij)
+    orc = oracle_for(scene, width, height, floor)
+    for (i, j), g in zip(ij.tolist(), got):
+        w = orc.dump(i, j)
+        assert (g["draw"], g["iters"], g["texel"], g["rgba"]) == \
+               (w["draw"], w["iters"], w["texel"], w["rgba"]), (i, j, g, w)
+        for k in ("xcoord", "ycoord", "brightness"):
+            assert abs(g[k] - w[k]) <= FLOAT_TOL, (i, j, k, g[k], w[k])
+        assert max(abs(a - b) for a, b in zip(g["pos"], w["pos"])) <= FLOAT_TOL, (i, j)
+
+
+def test_camera_outside_every_sphere(world, floor):
+    """largestDist == 0 on the first iteration: every pixel shades sphere 0 at cam.pos."""
+    scene = scenes.Scene("outside", np.array([[50, 0, 0, 2], [0, 40, 0, 3]], np.float32),
+                         cam_pos=(0.5, -0.25, 0.125))
+    world.set_scene(scene, 160, 96)
+    got = world.render()
+    want = oracle_for(scene, 160, 96, floor).render(1)
+    assert diff_report(got, want, 160) == ""
+
+
+def test_many_spheres_global_path(world, floor):
+    """n > 64 takes the device-buffer kernel (multi-word culling masks)."""
+    spheres = scenes.sort_spheres(scenes.lcg_spheres(count=199, seed=777))
+    scene = scenes.Scene("lcg200", spheres).posed(0.4, -0.1)
+    world.set_scene(scene, 640, 360)
+    got = world.render()
+    want = oracle_for(scene, 640, 360, floor).render(host_threads())
+    assert diff_report(got, want, 640) == ""
+
+
+def test_ragged_sizes(world, floor):
+    """Frame sizes that are not multiples of the 8x8 wave tile."""
+    scene = scenes.lcg64().posed(2.0, 0.4)
+    for width, height in [(1, 1), (7, 3), (333, 211), (1000, 9)]:
+        world.set_scene(scene, width, height)
+        got = world.render()
+        want = oracle_for(scene, width, height, floor).render(host_threads())
+        assert diff_report(got, want, width) == "", (width, height)
+
+
+def test_errors_fail_loudly(world):
+    import sfrt
+    with pytest.raises(sfrt.SfrtError) as e:
+        world.set_spheres(np.zeros((0, 4), np.float32))
+        world.render()
+    assert e.value.code == -2
+    with pytest.raises(sfrt.SfrtError):
+        world.set_spheres(np.array([[0, 0, 0, -1]], np.float32))
+    with pytest.raises(sfrt.SfrtError):
+        world.set_spheres(np.array([[0, 0, np.nan, 1]], np.float32))
+
+
+@pytest.mark.parametrize("fn,arg", [("asinf", "1"), ("atanf", "1"), ("atan2f", "100000000"),
+                                    ("sqrt_div", "16")])
+def test_device_math_matches_libm(fn, arg, tmp_path):
+    """sfrt_math on gfx950 vs host glibc: every binary32 input (atanf, asinf)."""
+    exe = tmp_path / "math_gpu_check"
+    src = os.path.join(ROOT, "tests", "native", "math_gpu_check.hip")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-ffp-contract=off", "-fopenmp", src, "-o", str(exe)], check=True,
+                   capture_output=True)
+    env = dict(os.environ, OMP_NUM_THREADS=str(host_threads()))
+    r = subprocess.run([str(exe), fn, arg], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
