@@ -44,6 +44,40 @@ def band_of(rank: int, world: int, height: int) -> tuple[int, int]:
     return r0, (rank + 1) * height // world - r0
 
 
+def band_buffers(rank: int, world_size: int, height: int, pitch: int, device):
+    """Row-band buffers for one frame of `height` rows.  Rank 0 owns the whole
+    frame and renders its band in place; the gather lands every other band in
+    its slice of the frame (views, no extra copy).  Returns (band buffer,
+    frame or None, gather list or None)."""
+    row0, rows = band_of(rank, world_size, height)
+    if world_size == 1:
+        frame = torch.empty(height, pitch, dtype=torch.uint8, device=device)
+        return frame, frame, None
+    if rank == 0:
+        frame = torch.empty(height, pitch, dtype=torch.uint8, device=device)
+        views = []
+        for r in range(world_size):
+            r0, n = band_of(r, world_size, height)
+            views.append(frame[r0:r0 + n])
+        return frame[row0:row0 + rows], frame, views
+    return torch.empty(rows, pitch, dtype=torch.uint8, device=device), None, None
+
+
+def gather_bands(buf, gather_list, rank: int, world_size: int, height: int) -> None:
+    """Bands -> rank 0.  Equal bands (height % world_size == 0): one gather
+    collective (RCCL over xGMI on the GPU node); otherwise one batch of
+    point-to-point transfers straight into the frame's row slices."""
+    if height % world_size == 0:
+        dist.gather(buf, gather_list, dst=0)
+        return
+    if rank == 0:
+        ops = [dist.P2POp(dist.irecv, gather_list[r], r) for r in range(1, world_size)]
+    else:
+        ops = [dist.P2POp(dist.isend, buf, 0)]
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+
+
 def time_frames(world, buf, pitch, row0, rows, steps, warmup, stream, gather=None):
     """Warmup, then `steps` timed frames.  Returns (wall seconds, kernel ms per frame)."""
     for _ in range(warmup):
@@ -121,22 +155,9 @@ def main() -> None:
     w.load_texture(*floor)
     w.set_scene(scene, WIDTH, height)
 
-    if world_size > 1:
-        band_rows = [band_of(r, world_size, height)[1] for r in range(world_size)]
-        if rank == 0:
-            frame = torch.empty(height, pitch, dtype=torch.uint8, device="cuda")
-            buf = frame[row0:row0 + rows]
-            gather_list = [frame[band_of(r, world_size, height)[0]:][:band_rows[r]]
-                           for r in range(world_size)]
-        else:
-            buf = torch.empty(rows, pitch, dtype=torch.uint8, device="cuda")
-            gather_list = None
-
-        def gather():
-            dist.gather(buf, gather_list, dst=0)
-    else:
-        buf = torch.empty(rows, pitch, dtype=torch.uint8, device="cuda")
-        gather = None
+    buf, frame, gather_list = band_buffers(rank, world_size, height, pitch, "cuda")
+    gather = ((lambda: gather_bands(buf, gather_list, rank, world_size, height))
+              if world_size > 1 else None)
 
     wall, kernel_ms = time_frames(w, buf, pitch, row0, rows, args.steps, args.warmup, stream,
                                   gather)
@@ -178,6 +199,13 @@ def main() -> None:
                                  "kernel time (HIP events on the launch stream); the kernel is "
                                  "VALU-bound, see DESIGN.md"},
         }
+    if world_size > 1 and rank == 0:
+        # The gathered frame must equal a single-GPU render of the whole frame.
+        single = torch.empty_like(frame)
+        w.render_band(single.data_ptr(), pitch, 0, height, stream.cuda_stream)
+        w.check(stream.cuda_stream)
+        result["gathered_frame_bit_identical"] = bool(torch.equal(single, frame))
+        del single
     if world_size == 1:
         # BASELINE config 2: 1920x1080, 10-sphere scene.
         w2 = sfrt.World(local_rank)

@@ -33,40 +33,27 @@ namespace sfrt_math {
 SFRT_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
 SFRT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 
-// s_atanf.c
+// s_atanf.c.  Written branch-free: every argument-reduction case keeps its
+// own operands, and the one division they need is shared (a/b with the same
+// a and b is the same correctly rounded value whichever case produced them),
+// so a wave whose lanes fall into different cases pays for one division.
 SFRT_HD float atanf(float x) {
   const uint32_t hx = f2u(x);
   const uint32_t ix = hx & 0x7fffffffu;
-  if (ix >= 0x4c000000u) {               // |x| >= 2^25 (or NaN / inf)
-    if (ix > 0x7f800000u) return x + x;  // NaN
-    if ((int32_t)hx > 0) return u2f(0x33a22168u) + u2f(0x3fc90fdau);  // atanlo[3] + atanhi[3]
-    return u2f(0xbfc90fdau) - u2f(0x33a22168u);                        // -atanhi[3] - atanlo[3]
-  }
-  int id;
-  if (ix < 0x3ee00000u) {                // |x| < 0.4375
-    if (ix < 0x31000000u) return x;      // |x| < 2^-29: huge + x > one holds
-    id = -1;
-  } else {
-    x = u2f(ix);                         // fabsf
-    if (ix < 0x3f980000u) {              // |x| < 1.1875
-      if (ix < 0x3f300000u) {            // 7/16 <= |x| < 11/16
-        id = 0;
-        x = ((x + x) - 1.0f) / (x + 2.0f);
-      } else {                           // 11/16 <= |x| < 19/16
-        id = 1;
-        x = (x - 1.0f) / (x + 1.0f);
-      }
-    } else {
-      if (ix < 0x401c0000u) {            // |x| < 2.4375
-        id = 2;
-        x = (x - 1.5f) / (x * 1.5f + 1.0f);
-      } else {                           // 2.4375 <= |x| < 2^25
-        id = 3;
-        x = -1.0f / x;
-      }
-    }
-  }
-  const float z = x * x;
+  const float ax = u2f(ix);  // fabsf
+  // id: -1 for |x| < 0.4375, 0..3 for the fdlibm reduction intervals
+  const int id = ix < 0x3ee00000u ? -1
+               : ix < 0x3f300000u ? 0    // 7/16 <= |x| < 11/16
+               : ix < 0x3f980000u ? 1    // 11/16 <= |x| < 19/16
+               : ix < 0x401c0000u ? 2    // 19/16 <= |x| < 39/16
+               : 3;                      // 39/16 <= |x| < 2^25
+  float num = x, den = 1.0f;             // id -1: x / 1 == x exactly
+  if (id == 0) { num = (ax + ax) - 1.0f; den = ax + 2.0f; }
+  if (id == 1) { num = ax - 1.0f; den = ax + 1.0f; }
+  if (id == 2) { num = ax - 1.5f; den = ax * 1.5f + 1.0f; }
+  if (id == 3) { num = -1.0f; den = ax; }
+  const float xr = num / den;
+  const float z = xr * xr;
   const float w = z * z;
   // aT[0,2,..,10] (odd-power terms) and aT[1,3,..,9] (even-power terms)
   float s1 = u2f(0x3c8569d7u) * w + u2f(0x3d4bda59u);   // aT10*w + aT8
@@ -80,20 +67,26 @@ SFRT_HD float atanf(float x) {
   s2 = s2 * w - u2f(0x3de38e38u);                      // aT3
   s2 = s2 * w - u2f(0x3e4ccccdu);                      // aT1
   s2 = s2 * w;
-  const float xs = (s1 + s2) * x;
-  if (id < 0) return x - xs;
-  float hi, lo;
-  switch (id) {
-    case 0: hi = u2f(0x3eed6338u); lo = u2f(0x31ac3769u); break;
-    case 1: hi = u2f(0x3f490fdau); lo = u2f(0x33222168u); break;
-    case 2: hi = u2f(0x3f7b985eu); lo = u2f(0x33140fb4u); break;
-    default: hi = u2f(0x3fc90fdau); lo = u2f(0x33a22168u); break;
+  const float xs = (s1 + s2) * xr;
+  float hi = u2f(0x3fc90fdau), lo = u2f(0x33a22168u);  // atanhi[3], atanlo[3]
+  if (id == 0) { hi = u2f(0x3eed6338u); lo = u2f(0x31ac3769u); }
+  if (id == 1) { hi = u2f(0x3f490fdau); lo = u2f(0x33222168u); }
+  if (id == 2) { hi = u2f(0x3f7b985eu); lo = u2f(0x33140fb4u); }
+  float r = hi - ((xs - lo) - xr);
+  r = (int32_t)hx < 0 ? -r : r;
+  if (id < 0) r = xr - xs;                  // |x| < 0.4375: x - x*(s1+s2)
+  if (ix < 0x31000000u) r = x;              // |x| < 2^-29: huge + x > one holds
+  if (ix >= 0x4c000000u) {                  // |x| >= 2^25, inf, NaN
+    r = (int32_t)hx > 0 ? u2f(0x33a22168u) + u2f(0x3fc90fdau)   // atanlo[3] + atanhi[3]
+                        : u2f(0xbfc90fdau) - u2f(0x33a22168u);  // -atanhi[3] - atanlo[3]
+    if (ix > 0x7f800000u) r = x + x;        // NaN
   }
-  const float r = hi - ((xs - lo) - x);
-  return (int32_t)hx < 0 ? -r : r;
+  return r;
 }
 
-// e_atan2f.c
+// e_atan2f.c, branch-free over the special cases.  The x == 1 shortcut of
+// the source (return atanf(y)) is folded into the general path: atanf is odd
+// and y/1 == y, so both give the same bits (checked exhaustively over y).
 SFRT_HD float atan2f(float y, float x) {
   const float tiny = u2f(0x0da24260u);    // 1.0e-30
   const float pi_o_4 = u2f(0x3f490fdbu);
@@ -102,51 +95,46 @@ SFRT_HD float atan2f(float y, float x) {
   const float m_pi_lo = u2f(0x33bbbd2eu); // -pi_lo = 8.7422776573e-08
   const uint32_t hx = f2u(x), hy = f2u(y);
   const uint32_t ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
-  if (ix > 0x7f800000u || iy > 0x7f800000u) return x + y;  // NaN
-  if (hx == 0x3f800000u) return sfrt_math::atanf(y);       // x == 1.0
   const int m = (int)((hy >> 31) | ((hx >> 30) & 2u));     // 2*sign(x) + sign(y)
-  if (iy == 0) {
-    switch (m) {
-      case 0:
-      case 1: return y;
-      case 2: return tiny + pi;
-      default: return -pi - tiny;
-    }
-  }
-  if (ix == 0) return (int32_t)hy < 0 ? -pi_o_2 - tiny : tiny + pi_o_2;
-  if (ix == 0x7f800000u) {
-    if (iy == 0x7f800000u) {
-      switch (m) {
-        case 0: return tiny + pi_o_4;
-        case 1: return -pi_o_4 - tiny;
-        case 2: return 3.0f * pi_o_4 + tiny;
-        default: return -3.0f * pi_o_4 - tiny;
-      }
-    }
-    switch (m) {
-      case 0: return 0.0f;
-      case 1: return -0.0f;
-      case 2: return tiny + pi;
-      default: return -pi - tiny;
-    }
-  }
-  if (iy == 0x7f800000u) return (int32_t)hy < 0 ? -pi_o_2 - tiny : tiny + pi_o_2;
   const int32_t d = (int32_t)iy - (int32_t)ix;
   const int32_t k = d >> 23;
-  float z;
-  if (d > 0x1e7fffff) {                       // |y/x| > 2^60
-    z = pi_o_2 - u2f(0x333bbd2eu);            // pi_o_2 + 0.5*pi_lo
-  } else if ((int32_t)hx < 0 && k < -60) {    // |y|/x < -2^60
-    z = 0.0f;
-  } else {
-    z = sfrt_math::atanf(u2f(f2u(y / x) & 0x7fffffffu));
+  float z = sfrt_math::atanf(u2f(f2u(y / x) & 0x7fffffffu));
+  if ((int32_t)hx < 0 && k < -60) z = 0.0f;  // |y|/x < -2^60
+  if (d > 0x1e7fffff) z = pi_o_2 - u2f(0x333bbd2eu);  // |y/x| > 2^60: pi_o_2 + 0.5*pi_lo
+  float r = m == 0 ? z
+          : m == 1 ? u2f(f2u(z) ^ 0x80000000u)
+          : m == 2 ? pi - (z + m_pi_lo)
+          : (z + m_pi_lo) - pi;
+  const float pm_pi_o_2 = (int32_t)hy < 0 ? -pi_o_2 - tiny : tiny + pi_o_2;
+  if (iy == 0x7f800000u) r = pm_pi_o_2;    // y = +-inf
+  if (ix == 0x7f800000u) {                 // x = +-inf
+    if (iy == 0x7f800000u) {
+      r = m == 0 ? tiny + pi_o_4 : m == 1 ? -pi_o_4 - tiny
+        : m == 2 ? 3.0f * pi_o_4 + tiny : -3.0f * pi_o_4 - tiny;
+    } else {
+      r = m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? tiny + pi : -pi - tiny;
+    }
   }
-  switch (m) {
-    case 0: return z;
-    case 1: return u2f(f2u(z) ^ 0x80000000u);
-    case 2: return pi - (z + m_pi_lo);
-    default: return (z + m_pi_lo) - pi;
-  }
+  if (ix == 0) r = pm_pi_o_2;              // x = 0
+  if (iy == 0) r = m <= 1 ? y : m == 2 ? tiny + pi : -pi - tiny;  // y = 0
+  if (ix > 0x7f800000u || iy > 0x7f800000u) r = x + y;  // NaN
+  return r;
+}
+
+// q / PI2 + 1.0f and q / PI + 0.5f (SphereWorld.cpp:373-374) without a
+// general division: q*(1/b) corrected by one exact residual (fma).  For every
+// FINITE binary32 q the final sums equal the reference's bits (exhaustive
+// check in tests/native/math_check.cpp; below 2^-104 the quotient itself may
+// differ but is absorbed by the + 1.0f / + 0.5f).
+SFRT_HD float div_pi2_plus_1(float q) {
+  const float b = 6.28318530718f, y = 1.0f / 6.28318530718f;
+  const float t = q * y;
+  return __builtin_fmaf(__builtin_fmaf(-t, b, q), y, t) + 1.0f;
+}
+SFRT_HD float div_pi_plus_half(float q) {
+  const float b = 3.1415926535f, y = 1.0f / 3.1415926535f;
+  const float t = q * y;
+  return __builtin_fmaf(__builtin_fmaf(-t, b, q), y, t) + 0.5f;
 }
 
 // e_asinf.c

@@ -18,6 +18,12 @@ constexpr int kMaskWords = kMaxSpheres / 64;
 constexpr int kTile = 8;              // one wave64 = one 8x8 pixel tile
 constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
 constexpr int kMaxIterations = 1 << 20;  // march guard; the reference has none
+// Per-wave culling is proven safe while every lane of the wave has made at
+// most this many march steps (the accumulated binary32 error of the march
+// positions stays below the culling margin, see cull_margin); a wave that
+// goes further switches to the full sphere list for the rest of its march.
+constexpr int kCullSafeIterations = 1024;
+constexpr int kSlots = 4;             // culled spheres held in SGPRs per wave (measured best of 0,4,6,8)
 
 // One sphere as the kernel reads it: 32 B, one s_load_dwordx8.
 struct SphereRec {
@@ -42,6 +48,7 @@ struct FrameRec {
   int tex_w, tex_h;
   float tex_wf, tex_hf;             // (float)texsize.x / .y (SphereWorld.cpp:376-377)
   int cull;                         // 1: per-wave cone culling (default), 0: every sphere
+  float cull_margin;                // absolute inflation of every sphere in the cone test
   long long out_pitch;              // output pitch in pixels
   uint32_t* out;                    // pixel (a, b) -> out[(b - sub_row0) * out_pitch + a]
   const uint32_t* tex;              // RGBA8 texels

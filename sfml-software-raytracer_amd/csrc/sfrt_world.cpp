@@ -194,6 +194,20 @@ struct sfrt_world {
     f.tex_wf = (float)(unsigned)tex_w[0];
     f.tex_hf = (float)(unsigned)tex_h[0];
     f.cull = cull;
+    // Culling margin (sphere_trace.hip, cull_mask).  A march step
+    // pos += dir * L rounds twice per component, so each step moves the
+    // position off the ray's exact line by at most ~2.1e-7 * (|pos| + L) <=
+    // 4.2e-7 * R, where R bounds every |coordinate| the march can reach (the
+    // camera and every sphere's |c| + r).  Over kCullSafeIterations (1024)
+    // steps that is < 4.3e-4 * R, inside the 1e-3 * R margin added to every
+    // radius; the reference test additionally needs r - |p - c| > 0.01.
+    const V3 origin{0.0f, 0.0f, 0.0f};
+    float reach = vlength(campos);
+    for (const sfrt_sphere& s : spheres) {
+      const float e = vlength(vsub(center(s), origin)) + s.radius;
+      reach = reach < e ? e : reach;
+    }
+    f.cull_margin = 1e-3f * reach + 1e-4f;
     f.tex = d_tex;
     f.status = d_status;
     recs.resize(spheres.size());

@@ -18,6 +18,8 @@
 //    (drawSphere, :368) and the max (:367) are unchanged.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "sfrt_math.h"
 #include "sfrt_trace.h"
 
@@ -29,15 +31,25 @@ namespace {
 constexpr float kPI = 3.1415926535f;     // SphereWorld.h:6
 constexpr float kPI2 = 6.28318530718f;   // SphereWorld.h:7
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Wave-wide minimum through DPP row ops (no LDS): min within each 16-lane
+// row, then the four row results via readlane.  Uniform result.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+      __builtin_bit_cast(int, x), __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
+
+__device__ __forceinline__ float wave_min(float v) {
+  v = fminf(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fminf(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fminf(v, dpp<0x141>(v));  // row_half_mirror
+  v = fminf(v, dpp<0x140>(v));  // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return fminf(fminf(r0, r1), fminf(r2, r3));
 }
 
 // Primary direction of pixel (i, j), normalised (SphereWorld.cpp:95-106, :358).
@@ -59,10 +71,10 @@ __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d,
                                          float py, float pz, PixelDump* dump) {
   float ang = d.atan_c - sfrt_math::atan2f(pz, px);
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
-  const float xcoord = ang / kPI2 + 1.0f;
+  const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
   const float ex = px - d.cx, ey = py - d.cy, ez = pz - d.cz;
   const float ny = ey / __builtin_sqrtf((ex * ex + ey * ey) + ez * ez);
-  const float ycoord = sfrt_math::asinf(ny) / kPI + 0.5f;
+  const float ycoord = sfrt_math::div_pi_plus_half(sfrt_math::asinf(ny));  // == asinf / PI + 0.5f
   const float bx = px - f.cam[0], by = py - f.cam[1], bz = pz - f.cam[2];
   const float bl = __builtin_sqrtf((bx * bx + by * by) + bz * bz);
   const float brightness = 3.0f / (bl < 3.0f ? 3.0f : bl);
@@ -95,40 +107,97 @@ __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d,
   return rgba;
 }
 
-// Wave-level cull: bit k of the result is set when sphere (base + k) can pass
-// the march test for some ray of this wave's tile.  Every lane holds one unit
-// ray (dx, dy, dz) of the tile.  A sphere is dropped only when the whole
-// cone around those rays misses the sphere inflated by a margin that covers
-// binary32 rounding of the march positions (|error| << 1e-3 * (|c-cam| + r)
-// for < 10^4 steps) -- inside that margin the reference test r - d > 0.01f
-// cannot hold.  Spheres whose threshold is 0 never pass and are dropped.
-__device__ __forceinline__ uint64_t cull_chunk(const FrameRec& f, const SphereRec* __restrict__ sph,
-                                               int base, double ax, double ay, double az,
-                                               double theta) {
-  const int lane = threadIdx.x & 63;
-  const int k = base + lane;
+// Cone of the wave's rays: unit axis through the tile centre, and the sine
+// and cosine of a half-angle that contains every lane's unit ray.  The sine
+// is taken from |d x a| (accurate for the small angles of a tile, unlike a
+// cosine near 1), maximised over the wave, plus slack for binary32 rounding.
+// A tile whose rays spread past ~60 degrees (strided subsets) gets wide = true
+// and is not culled.
+struct Cone {
+  float ax, ay, az, cos_t, sin_t;
+  bool wide;
+};
+
+__device__ __forceinline__ Cone tile_cone(const FrameRec& f, int tile_x, int tile_y, float dx,
+                                          float dy, float dz) {
+  const float ic = (float)f.xstart + ((float)(tile_x * kTile) + 3.5f) * (float)f.xadd;
+  const float jc = (float)f.ystart +
+                   ((float)(f.sub_row0 + tile_y * kTile) + 3.5f) * (float)f.yadd;
+  const float h = f.h_start + f.h_inc * ic;
+  const float v = f.v_start + jc * f.v_inc;
+  float ax = (f.fwd[0] + f.right[0] * h) + f.up[0] * v;
+  float ay = (f.fwd[1] + f.right[1] * h) + f.up[1] * v;
+  float az = (f.fwd[2] + f.right[2] * h) + f.up[2] * v;
+  const float inv = __builtin_amdgcn_rsqf((ax * ax + ay * ay) + az * az);
+  ax *= inv; ay *= inv; az *= inv;
+  const float cx = dy * az - dz * ay, cy = dz * ax - dx * az, cz = dx * ay - dy * ax;
+  const float sin_l = __builtin_sqrtf((cx * cx + cy * cy) + cz * cz);
+  const float cos_l = (dx * ax + dy * ay) + dz * az;
+  Cone c;
+  c.ax = ax; c.ay = ay; c.az = az;
+  c.sin_t = fminf(1.0f, -wave_min(-sin_l) + 1e-5f);
+  c.cos_t = __builtin_sqrtf(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
+  c.wide = wave_min(cos_l) < 0.5f;
+  return c;
+}
+
+// Wave-level cull ("wavefront ballot"): bit (k - base) of the result is set
+// when sphere k may pass the march test for some ray of this wave's tile.
+// Lane l tests sphere base + l against the cone.  A sphere is dropped only
+// when its distance to the cone exceeds its radius inflated by
+// f.cull_margin, which bounds how far the binary32 march positions can drift
+// from their rays (sfrt_world.cpp) -- there r - |p - c| > 0.01f cannot hold.
+// The distance from a centre at axial coordinate t and radial distance perp
+// to the cone's side line is perp * cos_t - t * sin_t; it is the distance to
+// the cone where the centre projects onto the side, and a lower bound of it
+// everywhere (behind the apex the distance is |w|).  Evaluating it in
+// binary32 errs by < 1e-6 |w|, covered by the 4e-6 |w| slack.  Spheres whose pass threshold is 0 never
+// pass and are dropped.
+__device__ __forceinline__ uint64_t cull_mask(const FrameRec& f, const SphereRec* __restrict__ sph,
+                                              int base, const Cone& c) {
+  const int k = base + (int)(threadIdx.x & 63);
   bool inc = false;
   if (k < f.n) {
     const SphereRec s = sph[k];
     if (s.s_pass > 0.0f) {
-      const double wx = (double)s.cx - (double)f.cam[0];
-      const double wy = (double)s.cy - (double)f.cam[1];
-      const double wz = (double)s.cz - (double)f.cam[2];
-      const double dist = sqrt(wx * wx + wy * wy + wz * wz);
-      const double rr = (double)s.r + 1e-3 * (dist + (double)s.r) + 1e-4;
-      if (dist <= rr) {
-        inc = true;
-      } else {
-        const double beta = asin(rr / dist);
-        const double c = fmin(1.0, fmax(-1.0, (wx * ax + wy * ay + wz * az) / dist));
-        inc = acos(c) <= theta + beta + 1e-6;
-      }
+      const float wx = s.cx - f.cam[0], wy = s.cy - f.cam[1], wz = s.cz - f.cam[2];
+      const float wl = __builtin_sqrtf((wx * wx + wy * wy) + wz * wz);
+      const float rr = s.r + f.cull_margin + 4e-6f * wl;
+      const float t = (wx * c.ax + wy * c.ay) + wz * c.az;
+      const float px = wx - t * c.ax, py = wy - t * c.ay, pz = wz - t * c.az;
+      const float perp = __builtin_sqrtf((px * px + py * py) + pz * pz);
+      // side distance, used where the centre projects onto the side (or
+      // within rr of that region: there it is still a lower bound)
+      const bool side = t * c.cos_t + perp * c.sin_t >= -rr;
+      inc = c.wide || wl <= rr || (side && perp * c.cos_t - t * c.sin_t <= rr);
     }
   }
   return __builtin_amdgcn_ballot_w64(inc);
 }
 
-template <bool INLINE>
+// One sphere test of the march (SphereWorld.cpp:365-369), exact: the pass
+// test is s < s_pass (see sfrt_world.cpp, pass_threshold) and sqrtf runs only
+// for a sphere that passes.
+__device__ __forceinline__ void sphere_step(float px, float py, float pz, float cx, float cy,
+                                            float cz, float r, float s_pass, int k, float& L,
+                                            int& dnew) {
+  const float ex = px - cx, ey = py - cy, ez = pz - cz;
+  const float ss = (ex * ex + ey * ey) + ez * ez;
+  const bool pass = ss < s_pass;
+  // Scalar branch around the sqrt: most culled spheres pass for no lane of
+  // the wave in a given step, and then the whole body is skipped (the
+  // compiler would otherwise if-convert it and run the sqrt every time).
+  if (__builtin_amdgcn_ballot_w64(pass)) {
+    __asm__ volatile("; sphere passes for some lane");  // keeps the branch (no if-conversion)
+    if (pass) {
+      const float t = r - __builtin_sqrtf(ss);
+      L = L < t ? t : L;  // std::max(largestDist, t)
+      dnew = k;
+    }
+  }
+}
+
+template <bool INLINE, int SLOTS>
 __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* __restrict__ sph) {
   __shared__ uint64_t s_mask[kWavesPerBlock][kMaskWords];
   const int lane = threadIdx.x & 63;
@@ -151,72 +220,113 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
   float dx, dy, dz;
   primary_dir(f, i, j, dx, dy, dz);
 
-  // ---- per-wave sphere cull (the "wavefront ballot") ----
-  const int nwords = (f.n + 63) >> 6;
-  uint64_t mask0 = ~0ull;
-  if (f.cull) {
-    const double ddx = dx, ddy = dy, ddz = dz;
-    double ax = wave_sum(ddx), ay = wave_sum(ddy), az = wave_sum(ddz);
-    const double an = sqrt(ax * ax + ay * ay + az * az);
-    ax /= an; ay /= an; az /= an;
-    const double dn = sqrt(ddx * ddx + ddy * ddy + ddz * ddz);
-    const double cmin = wave_min((ddx * ax + ddy * ay + ddz * az) / dn);
-    const double theta = acos(fmin(1.0, cmin)) + 1e-6;
-    if (INLINE) {
-      mask0 = cull_chunk(f, sph, 0, ax, ay, az, theta);
-    } else {
-      for (int w = 0; w < nwords; w++) {
-        const uint64_t m = cull_chunk(f, sph, w * 64, ax, ay, az, theta);
-        if (lane == 0) s_mask[wave][w] = m;
-      }
-    }
-  } else {
-    if (!INLINE && lane < nwords) {
-      const int rem = f.n - lane * 64;
-      s_mask[wave][lane] = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
-    }
-    if (INLINE) mask0 = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
-  }
-  if (!INLINE) __builtin_amdgcn_wave_barrier();
-
-  // ---- march, SphereWorld.cpp:362-372; iteration 1 (pos == cam) came from the host ----
   const float l0 = f.first_l;
   float px = f.cam[0] + dx * l0;
   float py = f.cam[1] + dy * l0;
   float pz = f.cam[2] + dz * l0;
   int draw = f.first_draw;
-  int iters = 1;
   bool active = valid && l0 > 0.0f;
-  while (__builtin_amdgcn_ballot_w64(active)) {
-    float L = 0.0f;
-    int dnew = draw;
-    for (int w = 0; w < (INLINE ? 1 : nwords); w++) {
-      uint64_t m = INLINE ? mask0 : s_mask[wave][w];
-      m = __builtin_amdgcn_readfirstlane((unsigned)m) |
-          ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32);
-      while (m) {
-        const int k = w * 64 + __builtin_ctzll(m);
+
+  // ---- per-wave sphere cull (the "wavefront ballot") ----
+  const int nwords = (f.n + 63) >> 6;
+  const bool any_march = __builtin_amdgcn_ballot_w64(active) != 0;
+  Cone cone{};
+  if (f.cull && any_march) cone = tile_cone(f, tile_x, tile_y, dx, dy, dz);
+  auto word_mask = [&](int w) -> uint64_t {
+    if (f.cull && any_march) return cull_mask(f, sph, w * 64, cone);
+    const int rem = f.n - w * 64;
+    return rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
+  };
+
+  if (INLINE) {
+    // ---- march with the culled spheres in SGPR slots ----
+    uint64_t m = any_march ? word_mask(0) : 0ull;
+    float scx[SLOTS + 1], scy[SLOTS + 1], scz[SLOTS + 1], sr[SLOTS + 1], ssp[SLOTS + 1];
+    int sk[SLOTS + 1];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < SLOTS; q++) {
+      scx[q] = scy[q] = scz[q] = sr[q] = ssp[q] = 0.0f;
+      sk[q] = 0;
+      if (m) {
+        const int k = __builtin_ctzll(m);
         m &= m - 1;
-        const SphereRec& s = sph[k];
-        const float ex = px - s.cx, ey = py - s.cy, ez = pz - s.cz;
-        const float ss = (ex * ex + ey * ey) + ez * ez;
-        if (ss < s.s_pass) {
-          const float t = s.r - __builtin_sqrtf(ss);
-          L = L < t ? t : L;  // std::max(largestDist, t)
-          dnew = k;
-        }
+        scx[q] = sph[k].cx; scy[q] = sph[k].cy; scz[q] = sph[k].cz;
+        sr[q] = sph[k].r; ssp[q] = sph[k].s_pass;
+        sk[q] = k;
+        cnt = q + 1;
       }
     }
-    if (active) {
-      px = px + dx * L;
-      py = py + dy * L;
-      pz = pz + dz * L;
-      draw = dnew;
-      ++iters;
-      active = L > 0.0f;
-      if (iters >= kMaxIterations) {
-        active = false;
-        atomicOr(f.status, 1);
+    uint64_t rest = m;  // culled spheres beyond the slots (higher indices)
+    int trips = 1;
+    while (__builtin_amdgcn_ballot_w64(active)) {
+      if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
+        cnt = 0;
+        rest = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
+      }
+      float L = 0.0f;
+      int dnew = draw;
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) {
+        if (q < cnt) sphere_step(px, py, pz, scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L, dnew);
+      }
+      for (uint64_t mm = rest; mm; mm &= mm - 1) {
+        const int k = __builtin_ctzll(mm);
+        const SphereRec& s = sph[k];
+        sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      }
+      if (active) {
+        px = px + dx * L;
+        py = py + dy * L;
+        pz = pz + dz * L;
+        draw = dnew;
+        active = L > 0.0f;
+      }
+      if (++trips >= kMaxIterations) {
+        if (active) atomicOr(f.status, 1);
+        break;
+      }
+    }
+  } else {
+    if (any_march) {
+      for (int w = 0; w < nwords; w++) {
+        const uint64_t m = word_mask(w);
+        if (lane == 0) s_mask[wave][w] = m;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    int trips = 1;
+    bool full = !(f.cull && any_march);
+    while (__builtin_amdgcn_ballot_w64(active)) {
+      if (trips == kCullSafeIterations) full = true;
+      float L = 0.0f;
+      int dnew = draw;
+      for (int w = 0; w < nwords; w++) {
+        uint64_t m;
+        if (full) {
+          const int rem = f.n - w * 64;
+          m = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
+        } else {
+          m = s_mask[wave][w];
+          m = __builtin_amdgcn_readfirstlane((unsigned)m) |
+              ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32);
+        }
+        for (; m; m &= m - 1) {
+          const int k = w * 64 + __builtin_ctzll(m);
+          const SphereRec& s = sph[k];
+          sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+        }
+      }
+      if (active) {
+        px = px + dx * L;
+        py = py + dy * L;
+        pz = pz + dz * L;
+        draw = dnew;
+        active = L > 0.0f;
+      }
+      if (++trips >= kMaxIterations) {
+        if (active) atomicOr(f.status, 1);
+        break;
       }
     }
   }
@@ -226,12 +336,13 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
   f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
 }
 
+template <int SLOTS>
 __global__ __launch_bounds__(256) void k_trace_inline(InlineArgs args) {
-  trace_tile<true>(args.f, args.s);
+  trace_tile<true, SLOTS>(args.f, args.s);
 }
 
 __global__ __launch_bounds__(256) void k_trace_global(FrameRec f) {
-  trace_tile<false>(f, f.spheres);
+  trace_tile<false, 0>(f, f.spheres);
 }
 
 // Debug/parity kernel: one lane per listed pixel, full sphere list, float
@@ -286,7 +397,18 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     InlineArgs args;
     args.f = f;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    hipLaunchKernelGGL(k_trace_inline, dim3((unsigned)blocks), dim3(256), 0, s, args);
+    // SFRT_SLOTS (tuning experiments only): culled spheres held in SGPRs.
+    static const int slots = [] {
+      const char* e = getenv("SFRT_SLOTS");
+      return e ? atoi(e) : kSlots;
+    }();
+    switch (slots) {
+      case 0: hipLaunchKernelGGL(k_trace_inline<0>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
+      case 4: hipLaunchKernelGGL(k_trace_inline<4>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
+      case 6: hipLaunchKernelGGL(k_trace_inline<6>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
+      case 8: hipLaunchKernelGGL(k_trace_inline<8>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
+      default: hipLaunchKernelGGL(k_trace_inline<kSlots>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
+    }
   } else {
     hipLaunchKernelGGL(k_trace_global, dim3((unsigned)blocks), dim3(256), 0, s, f);
   }

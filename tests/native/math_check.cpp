@@ -3,6 +3,8 @@
 //   g++ -O2 -std=c++17 -ffp-contract=off -fopenmp math_check.cpp -o math_check
 //   ./math_check asinf|atanf            -> every binary32 input
 //   ./math_check atan2f <npairs> <seed> -> random + structured pairs
+//   ./math_check atan2f_x1 | atan2f_y1  -> atan2f(y, 1) / atan2f(1, x) for every binary32
+//   ./math_check divpi                  -> q/PI2 + 1 and q/PI + 0.5 for every finite q
 // Prints "<fn> checked=<n> mismatches=<m>" and the first mismatches.
 #include <cmath>
 #include <cstdint>
@@ -37,6 +39,32 @@ int main(int argc, char** argv) {
           if (bad < 5) {
 #pragma omp critical
             printf("MISMATCH %s(%a [0x%08x]) libm=%a sfrt=%a\n", fn, x, bits(x), want, got);
+          }
+          bad++;
+        }
+      }
+    }
+  } else if (!strcmp(fn, "atan2f_x1") || !strcmp(fn, "atan2f_y1") || !strcmp(fn, "divpi")) {
+    const int mode = !strcmp(fn, "atan2f_x1") ? 0 : !strcmp(fn, "atan2f_y1") ? 1 : 2;
+#pragma omp parallel for reduction(+ : bad, checked) schedule(static)
+    for (long long hi = 0; hi < 65536; hi++) {
+      for (uint32_t lo = 0; lo < 65536; lo++) {
+        const float v = fl((uint32_t)(hi << 16) | lo);
+        bool ok;
+        if (mode == 0) {
+          ok = same(::atan2f(v, 1.0f), sfrt_math::atan2f(v, 1.0f));
+        } else if (mode == 1) {
+          ok = same(::atan2f(1.0f, v), sfrt_math::atan2f(1.0f, v));
+        } else {
+          if (!std::isfinite(v)) continue;
+          ok = same(v / 6.28318530718f + 1.0f, sfrt_math::div_pi2_plus_1(v)) &&
+               same(v / 3.1415926535f + 0.5f, sfrt_math::div_pi_plus_half(v));
+        }
+        checked++;
+        if (!ok) {
+          if (bad < 5) {
+#pragma omp critical
+            printf("MISMATCH %s(%a)\n", fn, v);
           }
           bad++;
         }

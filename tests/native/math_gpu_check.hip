@@ -4,6 +4,8 @@
 //   ./math_gpu_check asinf|atanf [stride]   -> every stride-th binary32 pattern
 //   ./math_gpu_check atan2f <npairs>        -> random + scene-range pairs
 //   ./math_gpu_check sqrt_div [stride]      -> correctly rounded sqrtf and x/y vs the host
+//   ./math_gpu_check divpi                  -> x/PI2 + 1 and x/PI + 0.5 (fma form) for every finite x
+//   ./math_gpu_check atan2f_x1              -> atan2f(y, 1) for every binary32 y
 // Prints "<fn> checked=<n> mismatches=<m>".
 #include <hip/hip_runtime.h>
 
@@ -28,7 +30,10 @@ __global__ void k_eval(int fn, const float* __restrict__ x, const float* __restr
     case 1: r = sfrt_math::atanf(x[i]); break;
     case 2: r = sfrt_math::atan2f(x[i], y[i]); break;
     case 3: r = __builtin_sqrtf(x[i]); break;
-    default: r = x[i] / y[i]; break;
+    case 4: r = x[i] / y[i]; break;
+    case 5: r = sfrt_math::div_pi2_plus_1(x[i]); break;
+    case 6: r = sfrt_math::div_pi_plus_half(x[i]); break;
+    default: r = sfrt_math::atan2f(x[i], 1.0f); break;
   }
   out[i] = r;
 }
@@ -39,7 +44,10 @@ static float host_eval(int fn, float x, float y) {
     case 1: return ::atanf(x);
     case 2: return ::atan2f(x, y);
     case 3: return std::sqrt(x);
-    default: return x / y;
+    case 4: return x / y;
+    case 5: return std::isfinite(x) ? x / 6.28318530718f + 1.0f : NAN;
+    case 6: return std::isfinite(x) ? x / 3.1415926535f + 0.5f : NAN;
+    default: return ::atan2f(x, 1.0f);
   }
 }
 
@@ -59,6 +67,8 @@ int main(int argc, char** argv) {
   else if (!strcmp(argv[1], "atanf")) fn = 1;
   else if (!strcmp(argv[1], "atan2f")) fn = 2;
   else if (!strcmp(argv[1], "sqrt_div")) fn = 3;
+  else if (!strcmp(argv[1], "divpi")) fn = 5;
+  else if (!strcmp(argv[1], "atan2f_x1")) fn = 7;
   else return 2;
   const long long total = fn == 2 ? (argc > 2 ? atoll(argv[2]) : 100000000LL)
                                   : (4294967296LL / (argc > 2 ? atoll(argv[2]) : 1));
@@ -71,9 +81,9 @@ int main(int argc, char** argv) {
     return 3;
   }
   unsigned long long checked = 0, bad = 0;
-  const int passes = fn == 3 ? 2 : 1;  // sqrt_div: pass 0 sqrtf, pass 1 division
+  const int passes = (fn == 3 || fn == 5) ? 2 : 1;  // sqrt_div: sqrtf, x/y; divpi: PI2, PI
   for (int pass = 0; pass < passes; pass++) {
-    const int f = fn == 3 ? 3 + pass : fn;
+    const int f = (fn == 3 || fn == 5) ? fn + pass : fn;
     for (long long base = 0; base < total; base += chunk) {
       const long n = (long)((total - base) < chunk ? (total - base) : chunk);
 #pragma omp parallel for schedule(static)
@@ -103,13 +113,15 @@ int main(int argc, char** argv) {
       for (long i = 0; i < n; i++) {
         const float want = host_eval(f, hx[i], hy[i]);
         const float got = hout[i];
-        const bool ok = (std::isnan(want) && std::isnan(got)) || bits(want) == bits(got);
+        const bool skip = (f == 5 || f == 6) && !std::isfinite(hx[i]);  // finite inputs only
+        const bool ok = skip || (std::isnan(want) && std::isnan(got)) || bits(want) == bits(got);
         if (!ok) b++;
       }
       if (b && bad < 1) {
         for (long i = 0; i < n; i++) {
           const float want = host_eval(f, hx[i], hy[i]);
-          if (!((std::isnan(want) && std::isnan(hout[i])) || bits(want) == bits(hout[i]))) {
+          const bool skip = (f == 5 || f == 6) && !std::isfinite(hx[i]);
+          if (!skip && !((std::isnan(want) && std::isnan(hout[i])) || bits(want) == bits(hout[i]))) {
             printf("MISMATCH fn=%d x=%a y=%a host=%a gpu=%a\n", f, hx[i], hy[i], want, hout[i]);
             break;
           }
