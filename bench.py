@@ -34,9 +34,24 @@ import scenes  # noqa: E402
 import sfrt  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-FP32_VALU_PEAK_TFLOPS = 157.3
+# VALU issue peak: 256 CUs x 4 SIMD32 x one wave64 instruction per 2 clocks at
+# 2.4 GHz = 1.229e12 wave-instructions/s (x 64 lanes = the 157.3 TFLOPS FP32
+# figure counted as FMA = 2).
+VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
 BYTES_PER_RAY = 4            # RGBA8 store; texture + sphere table are cache-resident
 WIDTH, ROWS_PER_GPU = 3840, 2160
+
+
+def measured_traffic(grid_threads: int):
+    """Per-launch HBM bytes and VALU instruction counts of this workload from the
+    newest profiles/*_traffic.json (tools/rocprof_summary.py over separate
+    rocprofv3 --pmc passes of this same command), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
+        ent = json.load(open(path))["per_grid_threads"].get(str(grid_threads))
+        if ent:
+            return ent, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def band_of(rank: int, world: int, height: int) -> tuple[int, int]:
@@ -197,8 +212,20 @@ def main() -> None:
                          "traffic": None,
                          "note": "algorithmic bytes = 4 B/ray (RGBA8 store) x rays per launch / "
                                  "kernel time (HIP events on the launch stream); the kernel is "
-                                 "VALU-bound, see DESIGN.md"},
+                                 "VALU-issue-bound, see valu_roofline and DESIGN.md"},
         }
+        meas, src = measured_traffic(rays_per_launch)
+        if meas:
+            result["roofline"]["traffic"] = round(meas["hbm_bytes_per_launch"])
+            result["roofline"]["traffic_source"] = src
+            if "SQ_INSTS_VALU" in meas:
+                rate = meas["SQ_INSTS_VALU"] / (kernel_ms * 1e-3)
+                result["valu_roofline"] = {
+                    "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTS / 1e12, 4),
+                    "unit": "T wave64-VALU-instructions/s", "frac": round(rate / VALU_PEAK_WAVE_INSTS, 4),
+                    "valu_insts_per_launch": round(meas["SQ_INSTS_VALU"]),
+                    "valu_insts_per_ray": round(meas["SQ_INSTS_VALU"] * 64 / rays_per_launch, 1),
+                    "source": src}
     if world_size > 1 and rank == 0:
         # The gathered frame must equal a single-GPU render of the whole frame.
         single = torch.empty_like(frame)
