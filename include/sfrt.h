@@ -117,8 +117,11 @@ SFRT_API int sfrt_world_check(sfrt_world* w, void* hip_stream);
 SFRT_API int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pixel_dump* out);
 
 /* Options: SFRT_OPT_CULL (1 = per-wave sphere culling, default; 0 = visit
- * every sphere -- same bytes, slower; used by A/B parity tests). */
+ * every sphere -- same bytes, slower; used by A/B parity tests).
+ * SFRT_OPT_VARIANT: kernel tuning variant for A/B timing (0 = default build;
+ * every variant produces the same bytes). */
 #define SFRT_OPT_CULL 1
+#define SFRT_OPT_VARIANT 2
 SFRT_API int sfrt_world_set_option(sfrt_world* w, int option, int value);
 
 /* ---- stateless helpers ---- */

@@ -49,6 +49,7 @@ struct FrameRec {
   float tex_wf, tex_hf;             // (float)texsize.x / .y (SphereWorld.cpp:376-377)
   int cull;                         // 1: per-wave cone culling (default), 0: every sphere
   float cull_margin;                // absolute inflation of every sphere in the cone test
+  int variant;                      // kernel variant for tuning A/B (0 = default)
   long long out_pitch;              // output pitch in pixels
   uint32_t* out;                    // pixel (a, b) -> out[(b - sub_row0) * out_pitch + a]
   const uint32_t* tex;              // RGBA8 texels

@@ -119,6 +119,7 @@ struct sfrt_world {
   int tex_w[SFRT_TEXTURE_SLOTS] = {};
   int tex_h[SFRT_TEXTURE_SLOTS] = {};
   int cull = 1;
+  int variant = 0;
   // --- device resources ---
   hipStream_t stream = nullptr;
   uint32_t* d_tex = nullptr;  // textures[0] on the device
@@ -194,6 +195,7 @@ struct sfrt_world {
     f.tex_wf = (float)(unsigned)tex_w[0];
     f.tex_hf = (float)(unsigned)tex_h[0];
     f.cull = cull;
+    f.variant = variant;
     // Culling margin (sphere_trace.hip, cull_mask).  A march step
     // pos += dir * L rounds twice per component, so each step moves the
     // position off the ray's exact line by at most ~2.1e-7 * (|pos| + L) <=
@@ -392,6 +394,10 @@ int sfrt_world_set_option(sfrt_world* w, int option, int value) {
   std::lock_guard<std::mutex> lk(w->mu);
   if (option == SFRT_OPT_CULL) {
     w->cull = value ? 1 : 0;
+    return SFRT_OK;
+  }
+  if (option == SFRT_OPT_VARIANT) {
+    w->variant = value;
     return SFRT_OK;
   }
   return SFRT_E_INVALID;

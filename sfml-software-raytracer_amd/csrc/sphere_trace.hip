@@ -18,7 +18,6 @@
 //    (drawSphere, :368) and the max (:367) are unchanged.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 
 #include "sfrt_math.h"
 #include "sfrt_trace.h"
@@ -52,6 +51,28 @@ __device__ __forceinline__ float wave_min(float v) {
   return fminf(fminf(r0, r1), fminf(r2, r3));
 }
 
+// sqrtf(x) correctly rounded for x >= 2^-96 (not denormal/tiny): the raw
+// v_sqrt_f32 (within 1 ulp) corrected by the two fma residual tests that the
+// compiler's own correctly rounded lowering uses -- minus its tiny-input
+// rescaling and special-value selects, which these inputs never need.
+__device__ __forceinline__ float sqrt_cr_normal(float x) {
+  const float r = __builtin_amdgcn_sqrtf(x);
+  const float rm = sfrt_math::u2f(sfrt_math::f2u(r) - 1u);
+  const float rp = sfrt_math::u2f(sfrt_math::f2u(r) + 1u);
+  float q = __builtin_fmaf(-rm, r, x) <= 0.0f ? rm : r;
+  q = __builtin_fmaf(-rp, r, x) > 0.0f ? rp : q;
+  return q;
+}
+
+constexpr float kTinySqrtArg = 0x1.0p-96f;
+
+// Correctly rounded sqrtf for any x: the short form unless some lane of the
+// wave has a tiny argument (then the compiler's full lowering for all lanes).
+__device__ __forceinline__ float sqrt_cr(float x) {
+  if (__builtin_amdgcn_ballot_w64(x < kTinySqrtArg)) return __builtin_sqrtf(x);
+  return sqrt_cr_normal(x);
+}
+
 // Primary direction of pixel (i, j), normalised (SphereWorld.cpp:95-106, :358).
 __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, float& dx,
                                             float& dy, float& dz) {
@@ -60,7 +81,8 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
   float x = (f.fwd[0] + f.right[0] * h) + f.up[0] * v;
   float y = (f.fwd[1] + f.right[1] * h) + f.up[1] * v;
   float z = (f.fwd[2] + f.right[2] * h) + f.up[2] * v;
-  const float len = __builtin_sqrtf((x * x + y * y) + z * z);
+  // |(x,y,z)|^2 >= 1 - tiny: forward is a unit vector orthogonal to right and up
+  const float len = sqrt_cr_normal((x * x + y * y) + z * z);
   dx = x / len;
   dy = y / len;
   dz = z / len;
@@ -73,10 +95,10 @@ __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d,
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
   const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
   const float ex = px - d.cx, ey = py - d.cy, ez = pz - d.cz;
-  const float ny = ey / __builtin_sqrtf((ex * ex + ey * ey) + ez * ez);
+  const float ny = ey / sqrt_cr((ex * ex + ey * ey) + ez * ez);
   const float ycoord = sfrt_math::div_pi_plus_half(sfrt_math::asinf(ny));  // == asinf / PI + 0.5f
   const float bx = px - f.cam[0], by = py - f.cam[1], bz = pz - f.cam[2];
-  const float bl = __builtin_sqrtf((bx * bx + by * by) + bz * bz);
+  const float bl = sqrt_cr((bx * bx + by * by) + bz * bz);
   const float brightness = 3.0f / (bl < 3.0f ? 3.0f : bl);
   // fmodf(v, 1.0f) == v - truncf(v) exactly for every binary32 v (NaN/inf -> NaN).
   float u = xcoord * 4.0f * d.r;
@@ -175,26 +197,39 @@ __device__ __forceinline__ uint64_t cull_mask(const FrameRec& f, const SphereRec
   return __builtin_amdgcn_ballot_w64(inc);
 }
 
-// One sphere test of the march (SphereWorld.cpp:365-369), exact: the pass
-// test is s < s_pass (see sfrt_world.cpp, pass_threshold) and sqrtf runs only
-// for a sphere that passes.
-__device__ __forceinline__ void sphere_step(float px, float py, float pz, float cx, float cy,
-                                            float cz, float r, float s_pass, int k, float& L,
-                                            int& dnew) {
-  const float ex = px - cx, ey = py - cy, ez = pz - cz;
-  const float ss = (ex * ex + ey * ey) + ez * ez;
-  const bool pass = ss < s_pass;
+// Pass body of a sphere test (SphereWorld.cpp:366-368) for the lanes in
+// `pass`: t = r - sqrtf(ss) exactly; largestDist = max; drawSphere = k.
+__device__ __forceinline__ void pass_body(bool pass, float ss, float r, int k, float& L,
+                                          int& dnew) {
   // Scalar branch around the sqrt: most culled spheres pass for no lane of
   // the wave in a given step, and then the whole body is skipped (the
   // compiler would otherwise if-convert it and run the sqrt every time).
   if (__builtin_amdgcn_ballot_w64(pass)) {
     __asm__ volatile("; sphere passes for some lane");  // keeps the branch (no if-conversion)
+    const bool tiny = __builtin_amdgcn_ballot_w64(pass && ss < kTinySqrtArg) != 0;
     if (pass) {
-      const float t = r - __builtin_sqrtf(ss);
+      const float d = tiny ? __builtin_sqrtf(ss) : sqrt_cr_normal(ss);
+      const float t = r - d;
       L = L < t ? t : L;  // std::max(largestDist, t)
       dnew = k;
     }
   }
+}
+
+// One sphere test of the march (SphereWorld.cpp:365-369), exact: the pass
+// test is s < s_pass (see sfrt_world.cpp, pass_threshold) and sqrtf runs only
+// for a sphere that passes.
+__device__ __forceinline__ float dist2(float px, float py, float pz, float cx, float cy,
+                                       float cz) {
+  const float ex = px - cx, ey = py - cy, ez = pz - cz;
+  return (ex * ex + ey * ey) + ez * ez;
+}
+
+__device__ __forceinline__ void sphere_step(float px, float py, float pz, float cx, float cy,
+                                            float cz, float r, float s_pass, int k, float& L,
+                                            int& dnew) {
+  const float ss = dist2(px, py, pz, cx, cy, cz);
+  pass_body(ss < s_pass, ss, r, k, L, dnew);
 }
 
 template <bool INLINE, int SLOTS>
@@ -243,7 +278,6 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
     uint64_t m = any_march ? word_mask(0) : 0ull;
     float scx[SLOTS + 1], scy[SLOTS + 1], scz[SLOTS + 1], sr[SLOTS + 1], ssp[SLOTS + 1];
     int sk[SLOTS + 1];
-    int cnt = 0;
 #pragma unroll
     for (int q = 0; q < SLOTS; q++) {
       scx[q] = scy[q] = scz[q] = sr[q] = ssp[q] = 0.0f;
@@ -254,22 +288,26 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
         scx[q] = sph[k].cx; scy[q] = sph[k].cy; scz[q] = sph[k].cz;
         sr[q] = sph[k].r; ssp[q] = sph[k].s_pass;
         sk[q] = k;
-        cnt = q + 1;
       }
     }
     uint64_t rest = m;  // culled spheres beyond the slots (higher indices)
     int trips = 1;
     while (__builtin_amdgcn_ballot_w64(active)) {
       if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
-        cnt = 0;
+#pragma unroll
+        for (int q = 0; q < SLOTS; q++) ssp[q] = 0.0f;  // slots never pass again
         rest = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
       }
       float L = 0.0f;
       int dnew = draw;
+      // Empty slots hold s_pass = 0 and never pass, so every slot is tested
+      // unconditionally: SLOTS independent dependency chains the scheduler
+      // can interleave, then the branches in index order.
+      float ssq[SLOTS + 1];
 #pragma unroll
-      for (int q = 0; q < SLOTS; q++) {
-        if (q < cnt) sphere_step(px, py, pz, scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L, dnew);
-      }
+      for (int q = 0; q < SLOTS; q++) ssq[q] = dist2(px, py, pz, scx[q], scy[q], scz[q]);
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) pass_body(ssq[q] < ssp[q], ssq[q], sr[q], sk[q], L, dnew);
       for (uint64_t mm = rest; mm; mm &= mm - 1) {
         const int k = __builtin_ctzll(mm);
         const SphereRec& s = sph[k];
@@ -397,17 +435,13 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     InlineArgs args;
     args.f = f;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    // SFRT_SLOTS (tuning experiments only): culled spheres held in SGPRs.
-    static const int slots = [] {
-      const char* e = getenv("SFRT_SLOTS");
-      return e ? atoi(e) : kSlots;
-    }();
-    switch (slots) {
-      case 0: hipLaunchKernelGGL(k_trace_inline<0>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
-      case 4: hipLaunchKernelGGL(k_trace_inline<4>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
-      case 6: hipLaunchKernelGGL(k_trace_inline<6>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
-      case 8: hipLaunchKernelGGL(k_trace_inline<8>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
-      default: hipLaunchKernelGGL(k_trace_inline<kSlots>, dim3((unsigned)blocks), dim3(256), 0, s, args); break;
+    // SFRT_OPT_VARIANT (tuning A/B only): number of SGPR sphere slots; 0 = kSlots.
+    const dim3 g((unsigned)blocks), b(256);
+    switch (f.variant) {
+      case 1: hipLaunchKernelGGL(k_trace_inline<0>, g, b, 0, s, args); break;
+      case 6: hipLaunchKernelGGL(k_trace_inline<6>, g, b, 0, s, args); break;
+      case 8: hipLaunchKernelGGL(k_trace_inline<8>, g, b, 0, s, args); break;
+      default: hipLaunchKernelGGL(k_trace_inline<kSlots>, g, b, 0, s, args); break;
     }
   } else {
     hipLaunchKernelGGL(k_trace_global, dim3((unsigned)blocks), dim3(256), 0, s, f);

@@ -19,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsfrt.so")
 
 SFRT_OPT_CULL = 1
+SFRT_OPT_VARIANT = 2
 ERRORS = {
     0: "SFRT_OK", -1: "SFRT_E_INVALID", -2: "SFRT_E_EMPTY", -3: "SFRT_E_NO_TEXTURE",
     -4: "SFRT_E_TOO_MANY", -5: "SFRT_E_HIP", -6: "SFRT_E_MARCH_LIMIT", -7: "SFRT_E_TEXEL",

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="march,nocull,outside,outside_nc")
+    ap.add_argument("--kvariants", default="0",
+                    help="comma list of SFRT_OPT_VARIANT values, interleaved per round")
     args = ap.parse_args()
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -60,10 +62,12 @@ def main():
             allv = (("march", sc, 1), ("nocull", sc, 0), ("outside", outside, 1),
                     ("outside_nc", outside, 0))
             for var, scene, cull in (v for v in allv if v[0] in args.variants.split(",")):
-                w.set_scene(scene, width, height)
-                w.set_option(sfrt.SFRT_OPT_CULL, cull)
-                med, best = time_kernel(w, buf, width, height, args.reps, stream)
-                out.setdefault(f"{name}/{var}", []).append(round(med * 1e3, 2))
+                for kv in [int(x) for x in args.kvariants.split(",")]:
+                    w.set_scene(scene, width, height)
+                    w.set_option(sfrt.SFRT_OPT_CULL, cull)
+                    w.set_option(sfrt.SFRT_OPT_VARIANT, kv)
+                    med, best = time_kernel(w, buf, width, height, args.reps, stream)
+                    out.setdefault(f"{name}/{var}/k{kv}", []).append(round(med * 1e3, 2))
     w.set_option(sfrt.SFRT_OPT_CULL, 1)
     for k, v in out.items():
         print(f"{k:32s} us(median per round) {v}")
