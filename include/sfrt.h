@@ -113,6 +113,19 @@ SFRT_API int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pit
                            int rows, void* hip_stream);
 SFRT_API int sfrt_world_check(sfrt_world* w, void* hip_stream);
 
+/* Pipelined frame fill for the display path: renders the
+ * whole width x height frame of the world's current state into `pixels`
+ * (width*height*4 bytes) without blocking, then copies it back while the
+ * caller submits the next frame (two frames in flight).  `pixels` should come
+ * from sfrt_host_alloc (pinned: the copy overlaps compute and runs at PCIe
+ * rate); it must stay valid until sfrt_world_wait_frame(ticket) returns, and
+ * then holds the same bytes sfrt_world_update_image(w, pixels, 0, 1, 0, 1)
+ * would have written.  The scene/camera are snapshotted at submit time. */
+SFRT_API int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket);
+SFRT_API int sfrt_world_wait_frame(sfrt_world* w, int64_t ticket);
+SFRT_API int sfrt_host_alloc(void** ptr, int64_t bytes);
+SFRT_API int sfrt_host_free(void* ptr);
+
 /* Float intermediates for `count` pixels (ij = i0, j0, i1, j1, ...), synchronous. */
 SFRT_API int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pixel_dump* out);
 

@@ -133,11 +133,33 @@ struct sfrt_world {
   size_t d_frame_px = 0;
   uint32_t* h_stage = nullptr;  // pinned D2H staging
   size_t h_stage_px = 0;
+  // --- frame pipeline (display path): render k+1 while frame k is copied ---
+  struct PipeSlot {
+    uint32_t* d_buf = nullptr;
+    size_t px = 0;
+    hipEvent_t rendered = nullptr, copied = nullptr;
+    int* d_status = nullptr;    // this frame's march/texel flags
+    int* h_status = nullptr;    // pinned copy, valid once `copied` completes
+    bool used = false;
+  };
+  static constexpr int kPipe = 2;
+  PipeSlot pipe[kPipe];
+  hipStream_t copy_stream = nullptr;
+  int64_t next_ticket = 0;
   std::mutex mu;
 
   ~sfrt_world() {
     DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+    for (PipeSlot& p : pipe) {
+      (void)hipFree(p.d_buf);
+      (void)hipFree(p.d_status);
+      (void)hipHostFree(p.h_status);
+      if (p.rendered) (void)hipEventDestroy(p.rendered);
+      if (p.copied) (void)hipEventDestroy(p.copied);
+    }
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     (void)hipFree(d_tex);
     (void)hipFree(d_status);
     for (auto* p : d_spheres) (void)hipFree(p);
@@ -525,6 +547,92 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
   (void)hipFree(d_ij);
   (void)hipFree(d_out);
   return rc ? rc : st;
+}
+
+int sfrt_host_alloc(void** ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) return SFRT_E_INVALID;
+  *ptr = nullptr;
+  return hipHostMalloc(ptr, (size_t)bytes, hipHostMallocDefault) == hipSuccess ? SFRT_OK
+                                                                               : SFRT_E_HIP;
+}
+
+int sfrt_host_free(void* ptr) {
+  if (!ptr) return SFRT_OK;
+  return hipHostFree(ptr) == hipSuccess ? SFRT_OK : SFRT_E_HIP;
+}
+
+int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
+  if (!w || !pixels || !ticket) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  int rc = w->validate();
+  if (rc) return rc;
+  DeviceGuard g(w->device);
+  if (!w->copy_stream && hipStreamCreateWithFlags(&w->copy_stream, hipStreamNonBlocking) != hipSuccess)
+    return SFRT_E_HIP;
+  const int64_t t = w->next_ticket;
+  sfrt_world::PipeSlot& slot = w->pipe[t % sfrt_world::kPipe];
+  if (!slot.rendered) {
+    HIP_TRY(hipEventCreateWithFlags(&slot.rendered, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&slot.copied, hipEventDisableTiming));
+    HIP_TRY(hipMalloc(&slot.d_status, sizeof(int)));
+    HIP_TRY(hipHostMalloc(&slot.h_status, sizeof(int), hipHostMallocDefault));
+  }
+  const size_t px = (size_t)w->width * w->height;
+  if (slot.px < px) {
+    if (slot.used) HIP_TRY(hipEventSynchronize(slot.copied));  // its last copy still reads d_buf
+    (void)hipFree(slot.d_buf);
+    slot.d_buf = nullptr;
+    HIP_TRY(hipMalloc(&slot.d_buf, px * 4));
+    slot.px = px;
+  }
+  // The slot's previous frame must have left d_buf before this render writes it.
+  if (slot.used) HIP_TRY(hipStreamWaitEvent(w->stream, slot.copied, 0));
+  HIP_TRY(hipMemsetAsync(slot.d_status, 0, sizeof(int), w->stream));
+  sfrt::FrameRec f;
+  std::vector<sfrt::SphereRec> recs;
+  w->prepare(f, recs);
+  f.xstart = 0; f.xadd = 1; f.ystart = 0; f.yadd = 1;
+  f.sub_w = w->width;
+  f.sub_row0 = 0;
+  f.sub_rows = w->height;
+  f.tiles_x = (w->width + sfrt::kTile - 1) / sfrt::kTile;
+  f.out = slot.d_buf;
+  f.out_pitch = w->width;
+  f.status = slot.d_status;
+  rc = w->stage_spheres(f, recs, w->stream, false);
+  if (rc) return rc;
+  if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
+  HIP_TRY(hipEventRecord(slot.rendered, w->stream));
+  HIP_TRY(hipStreamWaitEvent(w->copy_stream, slot.rendered, 0));
+  HIP_TRY(hipMemcpyAsync(pixels, slot.d_buf, px * 4, hipMemcpyDeviceToHost, w->copy_stream));
+  HIP_TRY(hipMemcpyAsync(slot.h_status, slot.d_status, sizeof(int), hipMemcpyDeviceToHost,
+                         w->copy_stream));
+  HIP_TRY(hipEventRecord(slot.copied, w->copy_stream));
+  slot.used = true;
+  *ticket = t;
+  w->next_ticket = t + 1;
+  return SFRT_OK;
+}
+
+int sfrt_world_wait_frame(sfrt_world* w, int64_t ticket) {
+  if (!w || ticket < 0) return SFRT_E_INVALID;
+  hipEvent_t ev;
+  int* h_status;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    if (ticket >= w->next_ticket) return SFRT_E_INVALID;
+    sfrt_world::PipeSlot& slot = w->pipe[ticket % sfrt_world::kPipe];
+    // A slot reused by a newer ticket records a later event on the same
+    // in-order copy stream, so waiting on it also covers this ticket.
+    ev = slot.copied;
+    h_status = slot.h_status;
+  }
+  DeviceGuard g(w->device);
+  HIP_TRY(hipEventSynchronize(ev));
+  const int st = *h_status;
+  if (st & 1) return SFRT_E_MARCH_LIMIT;
+  if (st & 2) return SFRT_E_TEXEL;
+  return SFRT_OK;
 }
 
 int sfrt_sort_spheres(sfrt_sphere* spheres, int count, const float cam_pos[3]) {

@@ -32,6 +32,7 @@ ABI_SYMBOLS = (
     "sfrt_world_add_sphere", "sfrt_world_set_spheres", "sfrt_world_get_spheres",
     "sfrt_world_update_spheres", "sfrt_world_update_image", "sfrt_world_render_band",
     "sfrt_world_check", "sfrt_world_trace_points", "sfrt_world_set_option",
+    "sfrt_world_submit_frame", "sfrt_world_wait_frame", "sfrt_host_alloc", "sfrt_host_free",
     "sfrt_sort_spheres", "sfrt_deg_to_rad", "sfrt_pass_threshold", "sfrt_error_string",
     "sfrt_version",
 )
@@ -99,6 +100,10 @@ def lib() -> ctypes.CDLL:
         "sfrt_world_check": ([W, vp], c_int),
         "sfrt_world_trace_points": ([W, vp, c_int, vp], c_int),
         "sfrt_world_set_option": ([W, c_int, c_int], c_int),
+        "sfrt_world_submit_frame": ([W, vp, P(ctypes.c_int64)], c_int),
+        "sfrt_world_wait_frame": ([W, ctypes.c_int64], c_int),
+        "sfrt_host_alloc": ([P(vp), ctypes.c_int64], c_int),
+        "sfrt_host_free": ([vp], c_int),
         "sfrt_sort_spheres": ([vp, c_int, vp], c_int),
         "sfrt_deg_to_rad": ([c_float], c_float),
         "sfrt_pass_threshold": ([c_float], c_float),
@@ -135,6 +140,29 @@ def deg_to_rad(deg: float) -> float:
 
 def pass_threshold(radius: float) -> float:
     return lib().sfrt_pass_threshold(float(radius))
+
+
+class HostFrame:
+    """Pinned host RGBA8 frame (sfrt_host_alloc), viewable as a numpy array."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        _check(lib().sfrt_host_alloc(ctypes.byref(p), int(nbytes)), "sfrt_host_alloc")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            lib().sfrt_host_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class World:
@@ -247,6 +275,19 @@ class World:
         _check(lib().sfrt_world_render_band(self._h, ctypes.c_void_p(dev_ptr), int(pitch_bytes),
                                             int(row0), int(rows), ctypes.c_void_p(stream or None)),
                "render_band")
+
+    def submit_frame(self, frame: "HostFrame") -> int:
+        """Pipelined full-frame fill into a pinned HostFrame; returns a ticket."""
+        w, h = self.size
+        if frame.nbytes < w * h * 4:
+            raise ValueError("host frame too small")
+        t = ctypes.c_int64()
+        _check(lib().sfrt_world_submit_frame(self._h, ctypes.c_void_p(frame.ptr), ctypes.byref(t)),
+               "submit_frame")
+        return t.value
+
+    def wait_frame(self, ticket: int) -> None:
+        _check(lib().sfrt_world_wait_frame(self._h, int(ticket)), "wait_frame")
 
     def check(self, stream: int = 0) -> None:
         _check(lib().sfrt_world_check(self._h, ctypes.c_void_p(stream or None)), "check")

@@ -203,3 +203,30 @@ def test_device_math_matches_libm(fn, arg, tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS=str(host_threads()))
     r = subprocess.run([str(exe), fn, arg], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
+
+
+def test_pipelined_frames_match_update_image(world, floor):
+    """Display path: two frames in flight, camera changing per frame."""
+    import sfrt
+    width, height = 640, 360
+    scene = scenes.lcg64()
+    poses = [(0.1 * k, 0.05 * (k % 3) - 0.05) for k in range(6)]
+    frames = [sfrt.HostFrame(width * height * 4) for _ in range(3)]
+    world.set_scene(scene, width, height)
+    tickets = []
+    for k, pose in enumerate(poses):
+        world.set_camera(scene.cam_pos, *pose)
+        tickets.append((world.submit_frame(frames[k % 3]), k))
+        if k >= 1:  # keep at most two frames in flight, check the older one
+            t, kk = tickets.pop(0)
+            world.wait_frame(t)
+            world.set_camera(scene.cam_pos, *poses[kk])
+            want = world.render()
+            world.set_camera(scene.cam_pos, *poses[k])
+            assert diff_report(frames[kk % 3].array, want, width) == "", kk
+    for t, kk in tickets:
+        world.wait_frame(t)
+        world.set_camera(scene.cam_pos, *poses[kk])
+        assert diff_report(frames[kk % 3].array, world.render(), width) == "", kk
+    for fr in frames:
+        fr.free()
