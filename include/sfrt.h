@@ -148,6 +148,60 @@ SFRT_API float sfrt_pass_threshold(float radius);
 SFRT_API const char* sfrt_error_string(int code);
 SFRT_API int sfrt_version(void);
 
+/* ======================================================================
+ * Voxel World frame fill: drop-in for
+ *   void World::UpdateImage(sf::Image* v, short ystart, short yadd,
+ *                           short xstart, short xadd)
+ *   (/root/reference/Raytracing/World.h:60, World.cpp:62-87; Raycast and
+ *   LRaycast World.cpp:302-491) over a snapshot of the World state.
+ * ====================================================================== */
+
+/* struct Dynamic (World.h:25-38): the fields Raycast reads. */
+typedef struct {
+  float pos[3];
+  float size[2];
+  float r, g, b;
+  float dist_to_camera;
+  int32_t texture_id; /* dynTextures slot */
+} sfrt_dynamic;
+
+/* struct Light (World.h:40-47). */
+typedef struct {
+  float pos[3];
+  float intensity, r, g, b;
+  int32_t shadows;
+} sfrt_light;
+
+typedef struct sfrt_voxel sfrt_voxel;
+
+#define SFRT_VOXEL_EMPTY (-32768)
+
+/* A new voxel world: 320x180, Camera defaults of World.h:9-19 (pos 15.5, 1.9,
+ * 15.5; fov 75/47 degrees converted like World.cpp:55-56), shadowDistance 16,
+ * viewDistance 24 (World.h:70-71), no blocks/textures/objects/lights. */
+SFRT_API int sfrt_voxel_create(int hip_device, sfrt_voxel** out);
+SFRT_API void sfrt_voxel_destroy(sfrt_voxel* v);
+SFRT_API int sfrt_voxel_set_size(sfrt_voxel* v, int width, int height);
+SFRT_API int sfrt_voxel_set_camera(sfrt_voxel* v, const sfrt_camera* cam);
+SFRT_API int sfrt_voxel_set_view(sfrt_voxel* v, float shadow_distance, float view_distance);
+/* `blocks` (World.h:75) as a dense grid: texture_ids[(x*ny + y)*nz + z] is
+ * Block::textureID (>= 0: textures[id]; < 0: colors[-id]) or SFRT_VOXEL_EMPTY;
+ * lookups keep the map's (x<<20)+(y<<10)+z key semantics. */
+SFRT_API int sfrt_voxel_set_blocks(sfrt_voxel* v, const int16_t* texture_ids, int nx, int ny, int nz);
+SFRT_API int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h);
+SFRT_API int sfrt_voxel_load_dyn_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h);
+SFRT_API int sfrt_voxel_set_colors(sfrt_voxel* v, const uint8_t* rgba, int count); /* colors[] */
+/* `dyn` in list order (World.h:93) and `alights` in list order (World.h:95). */
+SFRT_API int sfrt_voxel_set_dynamics(sfrt_voxel* v, const sfrt_dynamic* dyn, int count);
+SFRT_API int sfrt_voxel_set_lights(sfrt_voxel* v, const sfrt_light* lights, int count);
+/* World::UpdateImage into the caller's host RGBA8 frame; only addressed pixels written. */
+SFRT_API int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd, int xstart,
+                                     int xadd);
+/* Device row band [row0, row0+rows), asynchronous on hip_stream (NULL = null stream). */
+SFRT_API int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes, int row0,
+                                    int rows, void* hip_stream);
+SFRT_API int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -160,3 +160,75 @@ def add_spheres(adds, cam_pos=(0.0, 0.0, 0.0)) -> np.ndarray:
         n = lib().oracle_add_sphere(buf.ctypes.data_as(ctypes.POINTER(OracleSphere)), n,
                                     OracleSphere(*[float(v) for v in a]), cam)
     return buf[:n].copy()
+
+
+# ---- voxel World (voxelworld_oracle.c) ----
+class OvoxTexture(ctypes.Structure):
+    _fields_ = [("rgba", ctypes.c_void_p), ("w", ctypes.c_int32), ("h", ctypes.c_int32)]
+
+
+class OvoxScene(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("cam_pos", ctypes.c_float * 3),
+        ("cam_rotation", ctypes.c_float), ("cam_hrotation", ctypes.c_float),
+        ("fov_h", ctypes.c_float), ("fov_v", ctypes.c_float),
+        ("shadow_distance", ctypes.c_float), ("view_distance", ctypes.c_float),
+        ("blocks", ctypes.c_void_p), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
+        ("nz", ctypes.c_int32),
+        ("textures", OvoxTexture * 10), ("dyn_textures", OvoxTexture * 10),
+        ("colors", (ctypes.c_uint8 * 4) * 10),
+        ("dyn", ctypes.c_void_p), ("ndyn", ctypes.c_int32),
+        ("lights", ctypes.c_void_p), ("nlights", ctypes.c_int32),
+    ]
+
+
+class VoxelOracle:
+    """The voxel World restatement bound to one voxel_scenes.VoxelScene snapshot."""
+
+    def __init__(self, scene, width, height, textures, dyn_textures, colors):
+        L = lib()
+        L.ovox_render_threaded.argtypes = [ctypes.POINTER(OvoxScene), ctypes.c_void_p,
+                                           ctypes.c_int]
+        L.ovox_update_image.argtypes = [ctypes.POINTER(OvoxScene), ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.ovox_bad_texel_reads.restype = ctypes.c_long
+        self._keep = []
+        sc = OvoxScene()
+        sc.width, sc.height = int(width), int(height)
+        for k in range(3):
+            sc.cam_pos[k] = float(scene.cam_pos[k])
+        sc.cam_rotation, sc.cam_hrotation = float(scene.rotation), float(scene.hrotation)
+        sc.fov_h, sc.fov_v = float(scene.fov_h), float(scene.fov_v)
+        sc.shadow_distance, sc.view_distance = float(scene.shadow_distance), float(scene.view_distance)
+        blocks = np.ascontiguousarray(scene.blocks, dtype=np.int16)
+        sc.blocks = blocks.ctypes.data
+        sc.nx, sc.ny, sc.nz = blocks.shape
+        for slot, lst in (("textures", textures), ("dyn_textures", dyn_textures)):
+            arr = getattr(sc, slot)
+            for k, (rgba, w, h) in enumerate(lst):
+                buf = np.ascontiguousarray(rgba, dtype=np.uint8)
+                self._keep.append(buf)
+                arr[k].rgba, arr[k].w, arr[k].h = buf.ctypes.data, w, h
+        for k in range(min(10, len(colors))):
+            for c in range(4):
+                sc.colors[k][c] = int(colors[k][c])
+        dyn = np.ascontiguousarray(scene.dyn)
+        lights = np.ascontiguousarray(scene.lights)
+        sc.dyn, sc.ndyn = dyn.ctypes.data, dyn.shape[0]
+        sc.lights, sc.nlights = lights.ctypes.data, lights.shape[0]
+        self._keep += [blocks, dyn, lights]
+        self.scene = sc
+
+    def render(self, threads: int = 1) -> np.ndarray:
+        out = np.zeros(self.scene.width * self.scene.height * 4, dtype=np.uint8)
+        lib().ovox_render_threaded(ctypes.byref(self.scene), out.ctypes.data, int(threads))
+        return out
+
+    def update_image(self, out, ystart, yadd, xstart, xadd) -> None:
+        lib().ovox_update_image(ctypes.byref(self.scene), out.ctypes.data, ystart, yadd, xstart,
+                                xadd)
+
+    @staticmethod
+    def bad_texel_reads() -> int:
+        return int(lib().ovox_bad_texel_reads())

@@ -1,0 +1,405 @@
+// sfrt_voxel.cpp -- host side of the voxel World frame fill:
+// a C++ mirror of the state World::UpdateImage reads and the extern "C"
+// entry points sfrt_voxel_* of include/sfrt.h.
+//
+// Reference (paths under /root/reference/Raytracing/):
+//   class World                     World.h:58-97 (width/height 320x180, shadowDistance 16,
+//                                   viewDistance 24, Camera defaults World.h:9-19)
+//   World::World (fov -> radians)   World.cpp:55-56
+//   World::UpdateImage              World.cpp:62-87 (per-column / per-row terms below)
+//   blocks, textures, dynTextures,  World.h:75, 90-95
+//   colors, dyn, alights
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "sfrt.h"
+#include "sfrt_math.h"
+#include "voxel_trace.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kPI = 3.1415926535f;  // World.h:5
+
+#define HIP_TRY(expr)                            \
+  do {                                           \
+    if ((expr) != hipSuccess) return SFRT_E_HIP; \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// float -> unsigned as the reference's x86-64 build converts it.
+uint32_t to_u32(float f) {
+  if (!(f > -9.2233720368547758e18f && f < 9.2233720368547758e18f)) return 0u;
+  return (uint32_t)(int64_t)f;
+}
+
+struct DevTex {
+  uint32_t* d = nullptr;
+  int w = 0, h = 0;
+  size_t cap = 0;
+};
+
+int upload_texture(DevTex& t, const uint8_t* rgba, int w, int h) {
+  const size_t n = (size_t)w * h;
+  if (t.cap < n) {
+    (void)hipFree(t.d);
+    t.d = nullptr;
+    HIP_TRY(hipMalloc(&t.d, n * 4));
+    t.cap = n;
+  }
+  HIP_TRY(hipMemcpy(t.d, rgba, n * 4, hipMemcpyHostToDevice));
+  t.w = w;
+  t.h = h;
+  return SFRT_OK;
+}
+
+template <typename T>
+int upload_vector(T*& d, size_t& cap, const std::vector<T>& v, hipStream_t s) {
+  if (v.empty()) return SFRT_OK;
+  if (cap < v.size()) {
+    (void)hipFree(d);
+    d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(T) * v.size()));
+    cap = v.size();
+  }
+  // pageable source: staged by the runtime before the call returns
+  HIP_TRY(hipMemcpyAsync(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s));
+  return SFRT_OK;
+}
+
+}  // namespace
+
+struct sfrt_voxel {
+  int device = 0;
+  // --- World state read by UpdateImage ---
+  int width = 320, height = 180;            // World.h:67-68
+  sfrt_camera cam{};
+  float shadow_distance = 16.0f;            // World.h:70
+  float view_distance = 24.0f;              // World.h:71
+  std::vector<int16_t> blocks;
+  int nx = 0, ny = 0, nz = 0;
+  uint32_t colors[sfrt::kVoxSlots] = {};
+  std::vector<sfrt_dynamic> dyn;
+  std::vector<sfrt_light> lights;
+  // --- device resources ---
+  hipStream_t stream = nullptr;
+  DevTex tex[sfrt::kVoxSlots], dyn_tex[sfrt::kVoxSlots];
+  int16_t* d_blocks = nullptr;
+  size_t d_blocks_cap = 0;
+  bool blocks_dirty = true;
+  // per-frame arrays (stream-ordered reuse: every upload precedes its kernel on `stream`)
+  float* d_col = nullptr;
+  size_t d_col_cap = 0;
+  float* d_row = nullptr;
+  size_t d_row_cap = 0;
+  sfrt::VoxDyn* d_dyn = nullptr;
+  size_t d_dyn_cap = 0;
+  sfrt::VoxLight* d_lights = nullptr;
+  size_t d_lights_cap = 0;
+  int* d_status = nullptr;
+  uint32_t* d_frame = nullptr;
+  size_t d_frame_px = 0;
+  std::mutex mu;
+
+  ~sfrt_voxel() {
+    DeviceGuard g(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& t : tex) (void)hipFree(t.d);
+    for (auto& t : dyn_tex) (void)hipFree(t.d);
+    (void)hipFree(d_blocks);
+    (void)hipFree(d_col);
+    (void)hipFree(d_row);
+    (void)hipFree(d_dyn);
+    (void)hipFree(d_lights);
+    (void)hipFree(d_status);
+    (void)hipFree(d_frame);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  // Builds the frame record and uploads the per-frame arrays on stream s.
+  // Everything the reference recomputes per pixel but that depends only on the
+  // column, the row or the object is evaluated here, with its expressions.
+  int prepare(sfrt::VoxFrame& f, hipStream_t s) {
+    if (blocks.empty()) return SFRT_E_EMPTY;
+    if (width <= 0 || height <= 0) return SFRT_E_INVALID;
+    std::memset(&f, 0, sizeof f);
+    f.cam[0] = cam.pos[0]; f.cam[1] = cam.pos[1]; f.cam[2] = cam.pos[2];
+    f.view_distance = view_distance;
+    f.shadow_distance = shadow_distance;
+    f.maxiter = to_u32(view_distance * 1.5f);                       // World.cpp:322
+    // World.cpp:64-87
+    const float vStart = cam.fov_v / 2;
+    const float vIncreaseBy = cam.fov_v / height;
+    const float vOff = std::sin(cam.hrotation);
+    const float hStart = cam.rotation - cam.fov_h / 2;
+    const float hIncreaseBy = cam.fov_h / width;
+    std::vector<float> col((size_t)width * 3), row((size_t)height * 2);
+    for (int i = 0; i < width; i++) {
+      const float hray = (hStart + hIncreaseBy * i);
+      const float fix = std::cos(cam.rotation - hray);
+      const float dx = std::sin(hray) / fix, dz = std::cos(hray) / fix;
+      col[3 * (size_t)i] = dx;
+      col[3 * (size_t)i + 1] = dz;
+      col[3 * (size_t)i + 2] = sfrt_math::atan2f(dz, dx);  // VAngleXZ's ray term (World.cpp:272)
+    }
+    for (int j = 0; j < height; j++) {
+      const float vray = (vStart - j * vIncreaseBy);
+      row[2 * (size_t)j] = (vOff + std::sin(vray));
+      row[2 * (size_t)j + 1] = std::cos(cam.hrotation + vray);   // r->yscale
+    }
+    std::vector<sfrt::VoxDyn> vd(dyn.size());
+    for (size_t k = 0; k < dyn.size(); k++) {
+      const sfrt_dynamic& d = dyn[k];
+      sfrt::VoxDyn& o = vd[k];
+      o.px = d.pos[0]; o.py = d.pos[1]; o.pz = d.pos[2];
+      o.sx = d.size[0]; o.sy = d.size[1];
+      o.r = d.r; o.g = d.g; o.b = d.b;
+      o.dist = d.dist_to_camera;
+      // VNormalizeXZ(d->pos - cam.pos) (World.cpp:282-285, 361)
+      const float ex = d.pos[0] - cam.pos[0], ez = d.pos[2] - cam.pos[2];
+      const float l = std::sqrt(ex * ex + ez * ez);
+      o.atan_b = sfrt_math::atan2f(ez / l, ex / l);
+      o.tex = d.texture_id;
+      o.pad = 0;
+    }
+    std::vector<sfrt::VoxLight> vl(lights.size());
+    for (size_t k = 0; k < lights.size(); k++) {
+      const sfrt_light& L = lights[k];
+      vl[k] = {L.pos[0], L.pos[1], L.pos[2], L.intensity, L.r, L.g, L.b, L.shadows, 0};
+    }
+    int rc;
+    if ((rc = upload_vector(d_col, d_col_cap, col, s)) || (rc = upload_vector(d_row, d_row_cap, row, s)) ||
+        (rc = upload_vector(d_dyn, d_dyn_cap, vd, s)) ||
+        (rc = upload_vector(d_lights, d_lights_cap, vl, s)))
+      return rc;
+    if (blocks_dirty) {
+      if (d_blocks_cap < blocks.size()) {
+        (void)hipFree(d_blocks);
+        d_blocks = nullptr;
+        HIP_TRY(hipMalloc(&d_blocks, blocks.size() * sizeof(int16_t)));
+        d_blocks_cap = blocks.size();
+      }
+      HIP_TRY(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
+                             hipMemcpyHostToDevice, s));
+      blocks_dirty = false;
+    }
+    f.col = d_col;
+    f.row = d_row;
+    f.blocks = d_blocks;
+    f.nx = nx; f.ny = ny; f.nz = nz;
+    for (int k = 0; k < sfrt::kVoxSlots; k++) {
+      f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};
+      f.dyn_tex[k] = {dyn_tex[k].d, dyn_tex[k].w, dyn_tex[k].h};
+      f.colors[k] = colors[k];
+    }
+    f.dyn = d_dyn;
+    f.ndyn = (int)dyn.size();
+    f.lights = d_lights;
+    f.nlights = (int)lights.size();
+    f.status = d_status;
+    return SFRT_OK;
+  }
+
+  int read_status(hipStream_t s) {
+    HIP_TRY(hipStreamSynchronize(s));
+    int st = 0;
+    HIP_TRY(hipMemcpy(&st, d_status, sizeof(int), hipMemcpyDeviceToHost));
+    if (st) HIP_TRY(hipMemset(d_status, 0, sizeof(int)));
+    return (st & 2) ? SFRT_E_TEXEL : SFRT_OK;
+  }
+};
+
+extern "C" {
+
+int sfrt_voxel_create(int hip_device, sfrt_voxel** out) {
+  if (!out) return SFRT_E_INVALID;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || hip_device < 0 || hip_device >= count)
+    return SFRT_E_HIP;
+  sfrt_voxel* v = new sfrt_voxel();
+  v->device = hip_device;
+  // Camera defaults (World.h:9-19) and the constructor's fov conversion (World.cpp:55-56).
+  v->cam.pos[0] = 15.5f; v->cam.pos[1] = 1.9f; v->cam.pos[2] = 15.5f;
+  v->cam.fov_h = 75.0f * (kPI / 180.0f);
+  v->cam.fov_v = 47.0f * (kPI / 180.0f);
+  DeviceGuard g(hip_device);
+  if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&v->d_status, sizeof(int)) != hipSuccess ||
+      hipMemset(v->d_status, 0, sizeof(int)) != hipSuccess) {
+    delete v;
+    return SFRT_E_HIP;
+  }
+  *out = v;
+  return SFRT_OK;
+}
+
+void sfrt_voxel_destroy(sfrt_voxel* v) { delete v; }
+
+int sfrt_voxel_set_size(sfrt_voxel* v, int width, int height) {
+  if (!v || width <= 0 || height <= 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  v->width = width;
+  v->height = height;
+  return SFRT_OK;
+}
+
+int sfrt_voxel_set_camera(sfrt_voxel* v, const sfrt_camera* cam) {
+  if (!v || !cam) return SFRT_E_INVALID;
+  for (float c : {cam->pos[0], cam->pos[1], cam->pos[2], cam->rotation, cam->hrotation,
+                  cam->fov_h, cam->fov_v})
+    if (!std::isfinite(c)) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  v->cam = *cam;
+  return SFRT_OK;
+}
+
+int sfrt_voxel_set_view(sfrt_voxel* v, float shadow_distance, float view_distance) {
+  if (!v || !std::isfinite(shadow_distance) || !std::isfinite(view_distance) || view_distance < 0)
+    return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  v->shadow_distance = shadow_distance;
+  v->view_distance = view_distance;
+  return SFRT_OK;
+}
+
+int sfrt_voxel_set_blocks(sfrt_voxel* v, const int16_t* texture_ids, int nx, int ny, int nz) {
+  // The reference keys blocks by (x << 20) + (y << 10) + z (World.cpp:10); a
+  // dense grid is exact for 0 <= x < 2048, 0 <= y, z < 1024.
+  if (!v || !texture_ids || nx <= 0 || ny <= 0 || nz <= 0 || nx > 2048 || ny > 1024 || nz > 1024)
+    return SFRT_E_INVALID;
+  const size_t n = (size_t)nx * ny * nz;
+  for (size_t k = 0; k < n; k++)
+    if (texture_ids[k] != sfrt::kVoxEmpty &&
+        (texture_ids[k] >= sfrt::kVoxSlots || texture_ids[k] <= -sfrt::kVoxSlots))
+      return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  v->blocks.assign(texture_ids, texture_ids + n);
+  v->nx = nx; v->ny = ny; v->nz = nz;
+  v->blocks_dirty = true;
+  return SFRT_OK;
+}
+
+int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h) {
+  if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  DeviceGuard g(v->device);
+  HIP_TRY(hipStreamSynchronize(v->stream));
+  return upload_texture(v->tex[slot], rgba, w, h);
+}
+
+int sfrt_voxel_load_dyn_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h) {
+  if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  DeviceGuard g(v->device);
+  HIP_TRY(hipStreamSynchronize(v->stream));
+  return upload_texture(v->dyn_tex[slot], rgba, w, h);
+}
+
+int sfrt_voxel_set_colors(sfrt_voxel* v, const uint8_t* rgba, int count) {
+  if (!v || !rgba || count < 0 || count > sfrt::kVoxSlots) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  for (int k = 0; k < count; k++) std::memcpy(&v->colors[k], rgba + 4 * k, 4);
+  return SFRT_OK;
+}
+
+int sfrt_voxel_set_dynamics(sfrt_voxel* v, const sfrt_dynamic* dyn, int count) {
+  if (!v || count < 0 || (count > 0 && !dyn)) return SFRT_E_INVALID;
+  for (int k = 0; k < count; k++)
+    if (dyn[k].texture_id < 0 || dyn[k].texture_id >= sfrt::kVoxSlots) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  v->dyn.assign(dyn, dyn + count);
+  return SFRT_OK;
+}
+
+int sfrt_voxel_set_lights(sfrt_voxel* v, const sfrt_light* lights, int count) {
+  if (!v || count < 0 || (count > 0 && !lights)) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  v->lights.assign(lights, lights + count);
+  return SFRT_OK;
+}
+
+int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd, int xstart,
+                            int xadd) {
+  if (!v || !pixels || ystart < 0 || xstart < 0 || yadd <= 0 || xadd <= 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  const int sub_w = xstart < v->width ? (v->width - xstart + xadd - 1) / xadd : 0;
+  const int sub_h = ystart < v->height ? (v->height - ystart + yadd - 1) / yadd : 0;
+  if (v->blocks.empty()) return SFRT_E_EMPTY;
+  if (sub_w == 0 || sub_h == 0) return SFRT_OK;
+  DeviceGuard g(v->device);
+  const size_t px = (size_t)sub_w * sub_h;
+  if (v->d_frame_px < px) {
+    (void)hipFree(v->d_frame);
+    v->d_frame = nullptr;
+    HIP_TRY(hipMalloc(&v->d_frame, px * 4));
+    v->d_frame_px = px;
+  }
+  sfrt::VoxFrame f;
+  int rc = v->prepare(f, v->stream);
+  if (rc) return rc;
+  f.xstart = xstart; f.xadd = xadd; f.ystart = ystart; f.yadd = yadd;
+  f.sub_w = sub_w;
+  f.sub_row0 = 0;
+  f.sub_rows = sub_h;
+  f.out = v->d_frame;
+  f.out_pitch = sub_w;
+  if (sfrt::launch_voxel(f, v->stream)) return SFRT_E_HIP;
+  std::vector<uint32_t> stage(px);
+  HIP_TRY(hipMemcpyAsync(stage.data(), v->d_frame, px * 4, hipMemcpyDeviceToHost, v->stream));
+  rc = v->read_status(v->stream);
+  if (rc) return rc;
+  const size_t W = (size_t)v->width;
+  for (int b = 0; b < sub_h; b++) {
+    const size_t j = (size_t)ystart + (size_t)b * yadd;
+    for (int a = 0; a < sub_w; a++)
+      std::memcpy(pixels + (j * W + (size_t)xstart + (size_t)a * xadd) * 4, &stage[(size_t)b * sub_w + a], 4);
+  }
+  return SFRT_OK;
+}
+
+int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes, int row0, int rows,
+                           void* hip_stream) {
+  if (!v || !dev_pixels || row0 < 0 || rows < 0 || pitch_bytes % 4 != 0) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  if (pitch_bytes < (int64_t)v->width * 4 || row0 + rows > v->height) return SFRT_E_INVALID;
+  if (rows == 0) return SFRT_OK;
+  DeviceGuard g(v->device);
+  hipStream_t s = (hipStream_t)hip_stream;
+  sfrt::VoxFrame f;
+  int rc = v->prepare(f, s);
+  if (rc) return rc;
+  f.xstart = 0; f.xadd = 1; f.ystart = 0; f.yadd = 1;
+  f.sub_w = v->width;
+  f.sub_row0 = row0;
+  f.sub_rows = rows;
+  f.out = (uint32_t*)dev_pixels;
+  f.out_pitch = pitch_bytes / 4;
+  return sfrt::launch_voxel(f, s) ? SFRT_E_HIP : SFRT_OK;
+}
+
+int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream) {
+  if (!v) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  DeviceGuard g(v->device);
+  return v->read_status((hipStream_t)hip_stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// voxel_trace.h -- launch records shared by the voxel World host mirror
+// (sfrt_voxel.cpp) and its gfx950 kernel (voxel_trace.hip).  SURVEY 8f f2.
+//
+// Per-frame terms the reference recomputes per pixel with libm are computed
+// once on the host with the same expressions (World.cpp:62-87): per column
+// i the ray's x/z direction (sinf, cosf, the edge-distortion divide) and
+// atan2f(dir.z, dir.x) of VAngleXZ; per row j dir.y and r->yscale; per
+// dynamic object its VNormalizeXZ'd direction's atan2f.  The kernel needs no
+// transcendental.
+#pragma once
+
+#include <stdint.h>
+
+namespace sfrt {
+
+constexpr int kVoxSlots = 10;              // textures / dynTextures / colors (World.h:90-92)
+constexpr int16_t kVoxEmpty = -32768;
+
+struct VoxDyn {                             // struct Dynamic fields Raycast reads (World.h:25-38)
+  float px, py, pz;
+  float sx, sy;                             // size
+  float r, g, b;
+  float dist;                               // distToCamera
+  float atan_b;                             // atan2f of VNormalizeXZ(pos - cam.pos) (World.cpp:361)
+  int32_t tex;
+  int32_t pad;
+};
+
+struct VoxLight {                           // struct Light (World.h:40-47)
+  float px, py, pz;
+  float intensity, r, g, b;
+  int32_t shadows;
+  int32_t pad;
+};
+
+struct VoxTex {
+  const uint32_t* texels;                   // RGBA8
+  int32_t w, h;
+};
+
+struct VoxFrame {
+  float cam[3];
+  float view_distance, shadow_distance;
+  uint32_t maxiter;                         // (unsigned)(viewDistance * 1.5f), World.cpp:322
+  int32_t xstart, xadd, ystart, yadd;
+  int32_t sub_w, sub_row0, sub_rows;
+  const float* col;                         // per column i: dir.x, dir.z, atan2f(dir.z, dir.x)
+  const float* row;                         // per row j: dir.y, yscale
+  const int16_t* blocks;                    // dense [nx][ny][nz], textureID or kVoxEmpty
+  int32_t nx, ny, nz;
+  VoxTex tex[kVoxSlots];
+  VoxTex dyn_tex[kVoxSlots];
+  uint32_t colors[kVoxSlots];               // RGBA8 packed
+  const VoxDyn* dyn;
+  int32_t ndyn;
+  const VoxLight* lights;
+  int32_t nlights;
+  long long out_pitch;
+  uint32_t* out;
+  int* status;                              // bit 1: out-of-range texel read
+};
+
+int launch_voxel(const VoxFrame& f, void* stream);
+
+}  // namespace sfrt

@@ -1,0 +1,247 @@
+// voxel_trace.hip -- gfx950 kernel for the reference's voxel World frame fill
+// (SURVEY 8f row f2): World::Raycast / World::LRaycast,
+// /root/reference/Raytracing/World.cpp:302-491, one lane per pixel.
+//
+// Bit-exact with oracle/voxelworld_oracle.c: binary32 in the reference's
+// expression order, -ffp-contract=off, correctly rounded division and sqrt,
+// and the x86-64 float->integer conversions of the reference's build
+// (out-of-range and NaN give INT_MIN / 0) emulated explicitly.
+#include <hip/hip_runtime.h>
+
+#include "voxel_trace.h"
+
+#pragma clang fp contract(off)
+
+namespace sfrt {
+namespace {
+
+constexpr float kPI = 3.1415926535f;     // World.h:5
+constexpr float kPI2 = 6.28318530718f;   // World.h:6
+
+// x86-64 cvttss2si semantics (the reference's build): INT_MIN when out of range or NaN.
+__device__ __forceinline__ int32_t to_i32(float f) {
+  return (f > -2147483648.0f && f < 2147483648.0f) ? (int32_t)f : (int32_t)0x80000000;
+}
+// float -> unsigned as x86-64 g++ emits it: 64-bit cvttss2si, low 32 bits.
+__device__ __forceinline__ uint32_t to_u32(float f) {
+  if (!(f > -9.2233720368547758e18f && f < 9.2233720368547758e18f)) return 0u;
+  return (uint32_t)(long long)f;
+}
+__device__ __forceinline__ uint32_t to_u8(float f) {
+  return (uint32_t)to_i32(f) & 0xffu;
+}
+__device__ __forceinline__ float min255(float v) { return 255.0f < v ? 255.0f : v; }
+
+struct V3 {
+  float x, y, z;
+};
+
+// blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff
+// the key is non-negative and decodes to an occupied cell of the dense grid.
+__device__ __forceinline__ int16_t block_at(const VoxFrame& f, int32_t x, int32_t y, int32_t z) {
+  const int32_t key = (int32_t)(((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z);
+  if (key < 0) return kVoxEmpty;
+  const int32_t cx = key >> 20, cy = (key >> 10) & 1023, cz = key & 1023;
+  if (cx >= f.nx || cy >= f.ny || cz >= f.nz) return kVoxEmpty;
+  return f.blocks[((long long)cx * f.ny + cy) * f.nz + cz];
+}
+
+__device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, uint32_t x,
+                                          uint32_t y) {
+  const uint32_t idx = x + y * (uint32_t)t.w;
+  if (t.texels == nullptr || idx >= (uint32_t)(t.w * t.h)) {
+    atomicOr(f.status, 2);       // the reference reads outside the image here
+    return 0xffff00ffu;          // magenta, as the oracle
+  }
+  return t.texels[idx];
+}
+
+__device__ __forceinline__ uint32_t pack(uint32_t r, uint32_t g, uint32_t b, uint32_t a) {
+  return r | (g << 8) | (b << 16) | (a << 24);
+}
+
+// World::LRaycast, World.cpp:455-491.
+__device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
+  float dist = 0.0f;
+  int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
+  const float dirxadd = dir.x > 0 ? 1.0f : 0.0f, diryadd = dir.y > 0 ? 1.0f : 0.0f,
+              dirzadd = dir.z > 0 ? 1.0f : 0.0f;
+  const float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
+              sz = dir.z > 0 ? -1.0f : 1.0f;
+  const float lx = fabsf(dir.x), ly = fabsf(dir.y), lz = fabsf(dir.z);
+  const float m2 = maxDist * 2;
+  const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
+  for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
+    if (block_at(f, pix, piy, piz) != kVoxEmpty) return false;
+    const float a = (dirxadd + sx * (pos.x - (float)pix)) / lx;
+    const float b = (diryadd + sy * (pos.y - (float)piy)) / ly;
+    const float c = (dirzadd + sz * (pos.z - (float)piz)) / lz;
+    float raySpeed = a;  // std::min({a, b, c})
+    if (b < raySpeed) raySpeed = b;
+    if (c < raySpeed) raySpeed = c;
+    raySpeed += 0.002f;
+    dist += raySpeed;
+    pos.x = pos.x + dir.x * raySpeed;
+    pos.y = pos.y + dir.y * raySpeed;
+    pos.z = pos.z + dir.z * raySpeed;
+    pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
+  }
+  return dist >= maxDist;
+}
+
+// World::Raycast, World.cpp:302-453.
+__device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_dir) {
+  const V3 cam{f.cam[0], f.cam[1], f.cam[2]};
+  float dist = 0.0f;
+  V3 pos = cam;
+  int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
+  V3 tryPos = pos;
+  const float dirxadd = dir.x > 0 ? 1.0f : 0.0f, diryadd = dir.y > 0 ? 1.0f : 0.0f,
+              dirzadd = dir.z > 0 ? 1.0f : 0.0f;
+  float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
+        sz = dir.z > 0 ? -1.0f : 1.0f;   // dir*sign (short, exact as float)
+  const float lx = fabsf(dir.x), ly = fabsf(dir.y), lz = fabsf(dir.z);
+  int DI = 0;
+  float raySpeed = 0.0f;
+  int colRay = 0;
+  for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
+    const float xray = (dirxadd + sx * (pos.x - (float)pix)) / lx;
+    const float yray = (diryadd + sy * (pos.y - (float)piy)) / ly;
+    const float zray = (dirzadd + sz * (pos.z - (float)piz)) / lz;
+    if (xray <= yray && xray <= zray) {
+      raySpeed = xray;
+      tryPos.x += dir.x * (raySpeed + 0.002f);
+      tryPos.y += dir.y * raySpeed;
+      tryPos.z += dir.z * raySpeed;
+      colRay = 1;
+    } else if (yray <= xray && yray <= zray) {
+      raySpeed = yray;
+      tryPos.x += dir.x * raySpeed;
+      tryPos.y += dir.y * (raySpeed + 0.002f);
+      tryPos.z += dir.z * raySpeed;
+      colRay = 2;
+    } else {
+      raySpeed = zray;
+      tryPos.x += dir.x * raySpeed;
+      tryPos.y += dir.y * raySpeed;
+      tryPos.z += dir.z * (raySpeed + 0.002f);
+      colRay = 3;
+    }
+    const float tryDist = dist + raySpeed;
+
+    // dynamic billboards in front of the next block (World.cpp:353-378)
+    while (DI < f.ndyn && tryDist >= f.dyn[DI].dist) {
+      const VoxDyn& d = f.dyn[DI];
+      raySpeed = d.dist - dist;
+      dist = d.dist;
+      pos.x = pos.x + dir.x * raySpeed;
+      pos.y = pos.y + dir.y * raySpeed;
+      pos.z = pos.z + dir.z * raySpeed;
+      const float to = d.py - pos.y;
+      const float sizey = d.sy * yscale;
+      if (fabsf(to) < sizey) {
+        float ang = d.atan_b - atan_dir;  // VAngleXZ(dir, VNormalizeXZ(d->pos - cam.pos))
+        ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
+        ang = ang * dist;
+        const VoxTex& t = f.dyn_tex[d.tex];
+        const float xf = (0.5f + ang / kPI * 0.5f / d.sx);
+        if (xf > 0 && xf < 1) {
+          int32_t x = to_i32(xf * (float)(uint32_t)t.w);
+          int32_t y = to_i32((sizey + to) / sizey / 2 * (float)(uint32_t)t.h);
+          x = x < 0 ? 0 : x;
+          y = y < 0 ? 0 : y;
+          const uint32_t c = texel(f, t, (uint32_t)x, (uint32_t)y);
+          if ((c >> 24) > 127u) {
+            return pack(to_u8(min255((float)(c & 0xffu) * d.r)),
+                        to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
+                        to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
+          }
+        }
+      }
+      DI++;
+    }
+
+    dist = tryDist;
+    pos = tryPos;
+    pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
+    const int16_t id = block_at(f, pix, piy, piz);
+    if (id != kVoxEmpty) {  // hit a block (World.cpp:385)
+      uint32_t c;
+      if (id < 0) {
+        c = f.colors[-id];
+      } else {
+        const VoxTex& t = f.tex[id];
+        const float tw = (float)(uint32_t)t.w, th = (float)(uint32_t)t.h;
+        if (colRay == 1) {
+          c = texel(f, t, to_u32(tw * (pos.z - (float)piz)), to_u32(th * (pos.y - (float)piy)));
+          pos.x += sx * 0.01f;  // get it off the wall
+          sy = 0.0f;
+          sz = 0.0f;
+        } else if (colRay == 2) {
+          c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.z - (float)piz)));
+          pos.y += sy * 0.01f;
+          sx = 0.0f;
+          sz = 0.0f;
+        } else {
+          c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.y - (float)piy)));
+          pos.z += sz * 0.01f;
+          sx = 0.0f;
+          sy = 0.0f;
+        }
+      }
+      const float l0 = 0.05f / dist - dist * 0.0001f;
+      float litr = l0 < 0.0f ? 0.0f : l0;
+      float litg = litr, litb = litr;
+      for (int j = 0; j < f.nlights; j++) {
+        const VoxLight& L = f.lights[j];
+        const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
+        float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
+        float add = (L.intensity / dd - dd * 0.002f);
+        if (add > 0) {
+          float nx = L.px - pos.x, ny = L.py - pos.y, nz = L.pz - pos.z;
+          add *= ((nx * sx + ny * sy + nz * sz) * 0.7f + 0.3f);
+          if (add > 0) {
+            bool lit = true;
+            if (L.shadows && tryDist < f.shadow_distance) {
+              dd = __builtin_sqrtf(nx * nx + ny * ny + nz * nz);  // VLength
+              nx = nx / dd; ny = ny / dd; nz = nz / dd;
+              lit = lraycast(f, pos, V3{nx, ny, nz}, dd);
+            }
+            if (lit) {
+              litr += add * L.r;
+              litg += add * L.g;
+              litb += add * L.b;
+            }
+          }
+        }
+      }
+      return pack(to_u8(min255((float)(c & 0xffu) * litr)),
+                  to_u8(min255((float)((c >> 8) & 0xffu) * litg)),
+                  to_u8(min255((float)((c >> 16) & 0xffu) * litb)), c >> 24);
+    }
+  }
+  return pack(0, 0, 0, 255);  // sf::Color::Black
+}
+
+// 16x16 pixels per 256-thread workgroup.
+__global__ __launch_bounds__(256) void k_voxel(VoxFrame f) {
+  const int a = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int b = f.sub_row0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (a >= f.sub_w || b >= f.sub_row0 + f.sub_rows) return;
+  const int i = f.xstart + a * f.xadd;
+  const int j = f.ystart + b * f.yadd;
+  const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
+  const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2]);
+  f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
+}
+
+}  // namespace
+
+int launch_voxel(const VoxFrame& f, void* stream) {
+  if (f.sub_w <= 0 || f.sub_rows <= 0) return 0;
+  const dim3 grid((unsigned)((f.sub_w + 15) / 16), (unsigned)((f.sub_rows + 15) / 16));
+  hipLaunchKernelGGL(k_voxel, grid, dim3(256), 0, (hipStream_t)stream, f);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace sfrt

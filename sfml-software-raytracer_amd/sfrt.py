@@ -35,6 +35,11 @@ ABI_SYMBOLS = (
     "sfrt_world_submit_frame", "sfrt_world_wait_frame", "sfrt_host_alloc", "sfrt_host_free",
     "sfrt_sort_spheres", "sfrt_deg_to_rad", "sfrt_pass_threshold", "sfrt_error_string",
     "sfrt_version",
+    "sfrt_voxel_create", "sfrt_voxel_destroy", "sfrt_voxel_set_size", "sfrt_voxel_set_camera",
+    "sfrt_voxel_set_view", "sfrt_voxel_set_blocks", "sfrt_voxel_load_texture",
+    "sfrt_voxel_load_dyn_texture", "sfrt_voxel_set_colors", "sfrt_voxel_set_dynamics",
+    "sfrt_voxel_set_lights", "sfrt_voxel_update_image", "sfrt_voxel_render_band",
+    "sfrt_voxel_check",
 )
 
 
@@ -109,6 +114,20 @@ def lib() -> ctypes.CDLL:
         "sfrt_pass_threshold": ([c_float], c_float),
         "sfrt_error_string": ([c_int], ctypes.c_char_p),
         "sfrt_version": ([], c_int),
+        "sfrt_voxel_create": ([c_int, P(vp)], c_int),
+        "sfrt_voxel_destroy": ([vp], None),
+        "sfrt_voxel_set_size": ([vp, c_int, c_int], c_int),
+        "sfrt_voxel_set_camera": ([vp, P(Camera)], c_int),
+        "sfrt_voxel_set_view": ([vp, c_float, c_float], c_int),
+        "sfrt_voxel_set_blocks": ([vp, vp, c_int, c_int, c_int], c_int),
+        "sfrt_voxel_load_texture": ([vp, c_int, vp, c_int, c_int], c_int),
+        "sfrt_voxel_load_dyn_texture": ([vp, c_int, vp, c_int, c_int], c_int),
+        "sfrt_voxel_set_colors": ([vp, vp, c_int], c_int),
+        "sfrt_voxel_set_dynamics": ([vp, vp, c_int], c_int),
+        "sfrt_voxel_set_lights": ([vp, vp, c_int], c_int),
+        "sfrt_voxel_update_image": ([vp, vp, c_int, c_int, c_int, c_int], c_int),
+        "sfrt_voxel_render_band": ([vp, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
+        "sfrt_voxel_check": ([vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -305,3 +324,79 @@ class World:
                         "texel": list(d.texel),
                         "rgba": [rgba & 255, (rgba >> 8) & 255, (rgba >> 16) & 255, rgba >> 24]})
         return res
+
+
+class VoxelWorld:
+    """Device-backed mirror of the reference's voxel ``World`` frame fill
+    (World.h:58-97); the scene is a voxel_scenes.VoxelScene snapshot."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().sfrt_voxel_create(int(device), ctypes.byref(h)), "sfrt_voxel_create")
+        self._h = h
+        self.width = self.height = 0
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().sfrt_voxel_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def load_assets(self, textures, dyn_textures, colors) -> None:
+        for k, (rgba, w, h) in enumerate(textures):
+            buf = np.ascontiguousarray(rgba, dtype=np.uint8)
+            _check(lib().sfrt_voxel_load_texture(self._h, k, buf.ctypes.data, w, h), "load_texture")
+        for k, (rgba, w, h) in enumerate(dyn_textures):
+            buf = np.ascontiguousarray(rgba, dtype=np.uint8)
+            _check(lib().sfrt_voxel_load_dyn_texture(self._h, k, buf.ctypes.data, w, h),
+                   "load_dyn_texture")
+        col = np.ascontiguousarray(colors, dtype=np.uint8)
+        _check(lib().sfrt_voxel_set_colors(self._h, col.ctypes.data, col.shape[0]), "set_colors")
+
+    def set_scene(self, scene, width: int, height: int) -> None:
+        self.width, self.height = int(width), int(height)
+        _check(lib().sfrt_voxel_set_size(self._h, self.width, self.height), "set_size")
+        cam = Camera()
+        for k in range(3):
+            cam.pos[k] = float(scene.cam_pos[k])
+        cam.rotation, cam.hrotation = float(scene.rotation), float(scene.hrotation)
+        cam.fov_h, cam.fov_v = float(scene.fov_h), float(scene.fov_v)
+        _check(lib().sfrt_voxel_set_camera(self._h, ctypes.byref(cam)), "set_camera")
+        _check(lib().sfrt_voxel_set_view(self._h, float(scene.shadow_distance),
+                                         float(scene.view_distance)), "set_view")
+        b = np.ascontiguousarray(scene.blocks, dtype=np.int16)
+        _check(lib().sfrt_voxel_set_blocks(self._h, b.ctypes.data, *b.shape), "set_blocks")
+        d = np.ascontiguousarray(scene.dyn)
+        _check(lib().sfrt_voxel_set_dynamics(self._h, d.ctypes.data, d.shape[0]), "set_dynamics")
+        l = np.ascontiguousarray(scene.lights)
+        _check(lib().sfrt_voxel_set_lights(self._h, l.ctypes.data, l.shape[0]), "set_lights")
+
+    def update_image(self, pixels: np.ndarray, ystart=0, yadd=1, xstart=0, xadd=1) -> np.ndarray:
+        if pixels.dtype != np.uint8 or pixels.size != self.width * self.height * 4:
+            raise ValueError("pixels must be uint8 width*height*4")
+        _check(lib().sfrt_voxel_update_image(self._h, pixels.ctypes.data, ystart, yadd, xstart,
+                                             xadd), "voxel_update_image")
+        return pixels
+
+    def render(self) -> np.ndarray:
+        return self.update_image(np.zeros(self.width * self.height * 4, np.uint8))
+
+    def render_band(self, dev_ptr: int, pitch_bytes: int, row0: int, rows: int,
+                    stream: int = 0) -> None:
+        _check(lib().sfrt_voxel_render_band(self._h, ctypes.c_void_p(dev_ptr), int(pitch_bytes),
+                                            int(row0), int(rows), ctypes.c_void_p(stream or None)),
+               "voxel_render_band")
+
+    def check(self, stream: int = 0) -> None:
+        _check(lib().sfrt_voxel_check(self._h, ctypes.c_void_p(stream or None)), "voxel_check")

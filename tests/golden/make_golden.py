@@ -71,6 +71,20 @@ def main():
                 out["dumps"][key] = [dict(o.dump(int(i), int(j)), i=int(i), j=int(j))
                                      for i, j in ij]
             print(key, ent["fnv1a64"], flush=True)
+    # voxel World, oracle/voxelworld_oracle.c
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import voxel_scenes as vs
+    from test_voxel import VOXEL_CASES, case_key
+    vtex = vs.load_textures()
+    out["voxel"] = {}
+    for case in VOXEL_CASES:
+        w, h, p, r, hr = case
+        o = oracle.VoxelOracle(vs.default_world(p, r, hr), w, h, vtex[0], vtex[1], vs.COLORS)
+        frame = o.render(threads)
+        out["voxel"][case_key(case)] = {"width": w, "height": h, "cam_pos": list(p),
+                                        "rotation": r, "hrotation": hr,
+                                        "fnv1a64": oracle.fnv1a64(frame)}
+        print("voxel", case_key(case), out["voxel"][case_key(case)]["fnv1a64"], flush=True)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=0, sort_keys=True)
 
