@@ -202,6 +202,55 @@ SFRT_API int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pit
                                     int rows, void* hip_stream);
 SFRT_API int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream);
 
+/* ======================================================================
+ * GLSL renderer: drop-in for the live GPU path
+ *   world.shader.setUniform(...)                (SphereWorld.cpp:214-238,
+ *                                                Source.cpp:143-146)
+ *   rt.draw(sp, &world.shader)                  (Source.cpp:150-153)
+ * i.e. rayShader.frag (/root/reference/Raytracing/rayShader.frag:1-179) run
+ * once per pixel of a width x height render target.  Semantics the shader
+ * leaves to the driver are fixed in DESIGN.md section 4b.
+ * ====================================================================== */
+
+#define SFRT_GLSL_MAX_SPHERES 100 /* uniform vec4 spheres[100] (rayShader.frag:6-8) */
+
+/* The shader's uniforms (rayShader.frag:1-11); `ground` is set separately. */
+typedef struct {
+  float campos[3];
+  float rotation[2]; /* (cam.rotation, cam.hrotation) */
+  float fov[2];      /* (fovH, fovV) in radians */
+  float size[2];     /* render-target size */
+  int32_t sphere_count, all_spheres_count, light_count;
+  float spheres[SFRT_GLSL_MAX_SPHERES][4]; /* xyz, radius: walls, lights, ospheres */
+  float uvs[SFRT_GLSL_MAX_SPHERES][4];
+  float lights[SFRT_GLSL_MAX_SPHERES][4];
+} sfrt_glsl_uniforms;
+
+typedef struct sfrt_glsl sfrt_glsl;
+
+/* A new shader instance: all uniforms zero (GLSL's initial uniform values),
+ * no ground texture. */
+SFRT_API int sfrt_glsl_create(int hip_device, sfrt_glsl** out);
+SFRT_API void sfrt_glsl_destroy(sfrt_glsl* g);
+/* setUniform("ground", t) with t.setRepeated(true), t.generateMipmap()
+ * (SphereWorld.cpp:52-57): RGBA8 rows, power-of-two sides. */
+SFRT_API int sfrt_glsl_set_ground(sfrt_glsl* g, const uint8_t* rgba, int w, int h);
+SFRT_API int sfrt_glsl_set_uniforms(sfrt_glsl* g, const sfrt_glsl_uniforms* u);
+SFRT_API int sfrt_glsl_get_uniforms(sfrt_glsl* g, sfrt_glsl_uniforms* u);
+/* sf::Shader::setUniform by name: "campos" (3 floats), "rotation", "fov",
+ * "size" (2), "spheres[k]", "uvs[k]", "lights[k]" (4); ints "sphereCount",
+ * "allSpheresCount", "lightCount".  Unknown names -> SFRT_E_INVALID. */
+SFRT_API int sfrt_glsl_set_uniform(sfrt_glsl* g, const char* name, const float* v, int n);
+SFRT_API int sfrt_glsl_set_uniform_int(sfrt_glsl* g, const char* name, int value);
+/* rt.draw: rows [row0, row0+rows) of a width x height target into device
+ * memory (row 0 = top of the image, as rt.getTexture().copyToImage()),
+ * asynchronous on hip_stream (NULL = null stream). */
+SFRT_API int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height,
+                            int64_t pitch_bytes, int row0, int rows, void* hip_stream);
+/* rt.draw + rt.getTexture().copyToImage() into a host RGBA8 buffer (synchronous). */
+SFRT_API int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height);
+SFRT_API int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -232,3 +232,67 @@ class VoxelOracle:
     @staticmethod
     def bad_texel_reads() -> int:
         return int(lib().ovox_bad_texel_reads())
+
+
+OGLSL_DUMP_FIELDS = [
+    ("dir", ctypes.c_float * 3), ("wall_pos", ctypes.c_float * 3), ("wall_dist", ctypes.c_float),
+    ("wall_sphere", ctypes.c_int32), ("march_steps", ctypes.c_int32),
+    ("ball_dist", ctypes.c_float), ("smooth_dist", ctypes.c_float),
+    ("checkstep", ctypes.c_int32), ("draw_sphere", ctypes.c_int32),
+    ("total_dist", ctypes.c_float), ("xcoord", ctypes.c_float), ("ycoord", ctypes.c_float),
+    ("brightness", ctypes.c_float), ("color", ctypes.c_float * 4),
+]
+
+
+class OglslDump(ctypes.Structure):
+    _fields_ = OGLSL_DUMP_FIELDS
+
+
+class GlslOracle:
+    """rayShader.frag restatement (oracle/glsl_oracle.c) for one uniform block
+    (a glsl_scenes.UNIFORM_DTYPE record) and one ground texture."""
+
+    def __init__(self, uniforms, ground, gw: int, gh: int):
+        L = lib()
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        L.oglsl_render.argtypes = [vp, vp, i, i, i, i, i, i, vp]
+        L.oglsl_render.restype = ctypes.c_long
+        L.oglsl_render_threaded.argtypes = [vp, vp, i, i, i, i, vp, i]
+        L.oglsl_render_threaded.restype = ctypes.c_long
+        L.oglsl_pixel.argtypes = [vp, vp, i, i, i, i, i, i, ctypes.POINTER(OglslDump)]
+        L.oglsl_march_steps.argtypes = [vp, i, i, vp, i]
+        self.u = np.ascontiguousarray(np.asarray(uniforms).reshape(()).copy())
+        self.ground = np.ascontiguousarray(ground, dtype=np.uint8)
+        self.gw, self.gh = int(gw), int(gh)
+
+    def _args(self):
+        return self.u.ctypes.data, self.ground.ctypes.data, self.gw, self.gh
+
+    def render(self, width: int, height: int, threads: int = 1) -> np.ndarray:
+        out = np.zeros(width * height * 4, dtype=np.uint8)
+        capped = lib().oglsl_render_threaded(*self._args(), width, height, out.ctypes.data,
+                                             int(threads))
+        if capped:
+            raise RuntimeError(f"{capped} pixels hit the march cap")
+        return out
+
+    def render_band(self, width: int, height: int, row0: int, rows: int) -> np.ndarray:
+        out = np.zeros(width * rows * 4, dtype=np.uint8)
+        capped = lib().oglsl_render(*self._args(), width, height, row0, rows, out.ctypes.data)
+        if capped:
+            raise RuntimeError(f"{capped} pixels hit the march cap")
+        return out
+
+    def pixel(self, width: int, height: int, i: int, row: int) -> dict:
+        d = OglslDump()
+        lib().oglsl_pixel(*self._args(), width, height, i, row, ctypes.byref(d))
+        out = {}
+        for name, _ in OGLSL_DUMP_FIELDS:
+            v = getattr(d, name)
+            out[name] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+    def march_steps(self, width: int, height: int, threads: int = 1) -> np.ndarray:
+        steps = np.zeros(width * height, dtype=np.int32)
+        lib().oglsl_march_steps(self.u.ctypes.data, width, height, steps.ctypes.data, int(threads))
+        return steps.reshape(height, width)

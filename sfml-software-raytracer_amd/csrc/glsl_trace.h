@@ -1,0 +1,66 @@
+// glsl_trace.h -- launch record shared by the GLSL-mode host mirror
+// (sfrt_glsl.cpp) and its gfx950 kernel (glsl_trace.hip).  SURVEY 8f row f1.
+//
+// rayShader.frag (/root/reference/Raytracing/rayShader.frag) recomputes per
+// fragment several terms that depend only on the uniforms; the host evaluates
+// them once per draw with the same expressions:
+//  * the camera basis of main() (:165-169, sin/cos) and fov.x / size.x * 2;
+//  * per wall sphere the exact squared-length bound of the containment test
+//    `step(length(rpos), r)` (:74), so the wall pass needs no sqrt to decide;
+//  * per (light, shadow ball) pair distance(light, ball), atan(r, distance)
+//    and the unit light->ball direction (:140-142).
+#pragma once
+
+#include <stdint.h>
+
+namespace sfrt {
+
+constexpr int kGlslMax = 100;          // uniform vec4 spheres[100] (rayShader.frag:6-8)
+constexpr int kGlslMipLevels = 16;
+constexpr int kGlslMarchCap = 1 << 20; // the shader has no cap; the status reports hitting it
+
+struct GlslWall {                      // spheres[0 .. sphereCount)
+  float x, y, z, r;
+  float rr;                            // r*r (:77)
+  float s_in;                          // step(sqrt(s), r) == 1  <=>  s <= s_in
+  float pad0, pad1;
+};
+
+struct GlslBall {                      // spheres[sphereCount .. allSpheresCount)
+  float x, y, z, r;
+};
+
+struct GlslPair {                      // light i, shadow ball j (:140-142)
+  float dist;                          // distance(spheres[i], spheres[j])
+  float sanglet;                       // atan(spheres[j].w, dist)
+  float ux, uy, uz;                    // (spheres[j] - spheres[i]) / dist
+  float bx, by, bz;                    // spheres[j].xyz
+};
+
+struct GlslMat {                       // per uniform index: uvs[k], lights[k], spheres[k].xyz
+  float uv[4];
+  float light[4];
+  float cx, cy, cz, pad;
+};
+
+struct GlslFrame {
+  float campos[3];
+  float fwd[3], right[3], up[3];
+  float fov_x, fov_y, hk, vk;          // hk = fov.x / size.x * 2 (:172), vk likewise
+  int32_t sc, lc, all;
+  int32_t width, height, row0, rows, tiles_x;
+  const GlslWall* walls;
+  const GlslBall* balls;               // all - sc entries (lights, then ospheres)
+  const GlslPair* pairs;               // [light][shadow ball], lc x (all - sc - lc)
+  const GlslMat* mats;                 // kGlslMax entries
+  const uint32_t* mip;                 // RGBA8 levels back to back
+  int32_t mip_levels;
+  int32_t mip_w[kGlslMipLevels], mip_h[kGlslMipLevels], mip_off[kGlslMipLevels];
+  long long out_pitch;                 // in pixels
+  uint32_t* out;
+  int* status;                         // bit 0: march cap reached
+};
+
+int launch_glsl(const GlslFrame& f, void* stream);
+
+}  // namespace sfrt

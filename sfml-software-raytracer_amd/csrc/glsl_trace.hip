@@ -1,0 +1,228 @@
+// glsl_trace.hip -- gfx950 kernel for the GLSL renderer:
+// one lane per fragment of rayShader.frag (/root/reference/Raytracing/
+// rayShader.frag:63-179), one wave64 per 8x8 tile, RGBA8 straight to HBM.
+//
+// The semantics the shader leaves to the OpenGL driver are fixed in DESIGN.md
+// section 4b (IEEE binary32 without contraction, correctly rounded / and
+// sqrt, glibc acosf, GLSL-spec min/max/mod/step/smoothstep, GL_NEAREST /
+// GL_NEAREST_MIPMAP_LINEAR sampling of the mipmapped REPEAT `ground`, unorm8
+// framebuffer rounding) and this kernel is held to the CPU restatement
+// (oracle/glsl_oracle.c) bit for bit.  Every expression keeps the shader's
+// operand order.  Sphere data are wave-uniform (scalar loads); only the
+// per-fragment lookups by drawSphere (:123-125, :154) are vector loads.
+#include <hip/hip_runtime.h>
+
+#include "glsl_trace.h"
+#include "sfrt_device.h"
+#include "sfrt_math.h"
+
+#pragma clang fp contract(off)
+
+namespace sfrt {
+namespace {
+
+// GLSL spec built-ins (min(x, y) = y < x ? y : x, ...), NaN behaviour included.
+__device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
+__device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
+__device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
+__device__ __forceinline__ float gmod(float x, float y) { return x - y * floorf(x / y); }
+
+__device__ __forceinline__ float len3(float x, float y, float z) {
+  return sqrt_cr((x * x + y * y) + z * z);
+}
+
+// Nearest texel of one level with REPEAT wrap, channels / 255.
+__device__ __forceinline__ void texel(const GlslFrame& f, int level, float s, float t, float& r,
+                                      float& g, float& b) {
+  const int w = f.mip_w[level], h = f.mip_h[level];
+  const float fu = floorf(s * (float)w), fv = floorf(t * (float)h);
+  const int i = fabsf(fu) < 16777216.0f ? ((int)fu & (w - 1)) : 0;  // w, h powers of two
+  const int j = fabsf(fv) < 16777216.0f ? ((int)fv & (h - 1)) : 0;
+  const uint32_t p = f.mip[f.mip_off[level] + j * w + i];
+  r = (float)(p & 255u) / 255.0f;
+  g = (float)((p >> 8) & 255u) / 255.0f;
+  b = (float)((p >> 16) & 255u) / 255.0f;
+}
+
+__device__ __forceinline__ uint32_t unorm8(float v) {
+  if (!(v > 0.0f)) return 0u;  // NaN too
+  if (!(v < 1.0f)) return 255u;
+  return (uint32_t)(int)floorf(v * 255.0f + 0.5f);
+}
+
+__device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
+  const float fx = (float)i + 0.5f;
+  const float fy = (float)(f.height - 1 - row) + 0.5f;
+  const float ax = -f.fov_x + f.hk * fx;                                   // :172-173
+  const float ay = -f.fov_y + f.vk * fy;
+  float dx = (f.fwd[0] + f.right[0] * ax) + f.up[0] * ay;                 // :175
+  float dy = (f.fwd[1] + f.right[1] * ax) + f.up[1] * ay;
+  float dz = (f.fwd[2] + f.right[2] * ax) + f.up[2] * ay;
+  {
+    const float l = len3(dx, dy, dz);                                     // :65
+    dx = dx / l;
+    dy = dy / l;
+    dz = dz / l;
+  }
+  const float cx = f.campos[0], cy = f.campos[1], cz = f.campos[2];
+
+  // ---- furthest wall: 3 passes over the walls (:71-85) ----
+  float px = cx, py = cy, pz = cz;
+  int draw = 0;
+  float total = 0.0f;
+  for (int j = 0, k = 0; j < 3 * f.sc; j++) {
+    const GlslWall w = f.walls[k];
+    const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
+    const float s = (rx * rx + ry * ry) + rz * rz;
+    const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
+    float tosurf = 0.0f;                               // the step-0 value: 0 * (...) * 0.5 == +0
+    if (__builtin_amdgcn_ballot_w64(inside)) {
+      const float cs = inside ? 1.0f : 0.0f;
+      const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
+      const float c = cs * s - w.rr;
+      tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
+    }
+    draw = inside ? k : draw;
+    px = px + dx * tosurf;
+    py = py + dy * tosurf;
+    pz = pz + dz * tosurf;
+    total = total + tosurf;
+    if (++k == f.sc) k = 0;
+  }
+
+  // ---- metaball march over lights + ospheres (:87-112) ----
+  const int nballs = f.all - f.sc;
+  float ball_dist = 0.0f;
+  float smooth = 999999999.0f;
+  int closest = 0;
+  float snx = 0.0f, sny = 0.0f, snz = 0.0f;
+  int steps = 0;
+  while (ball_dist < total && smooth > 0.01f) {
+    if (++steps > kGlslMarchCap) {
+      atomicOr(f.status, 1);
+      break;
+    }
+    const float tx = cx + dx * ball_dist, ty = cy + dy * ball_dist, tz = cz + dz * ball_dist;
+    smooth = 999999999.0f;
+    closest = 0;
+    float shortest = 9999999.0f;
+    snx = sny = snz = 0.0f;
+    for (int k = 0; k < nballs; k++) {
+      const GlslBall b = f.balls[k];
+      const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
+      const float other = len3(ox, oy, oz) - b.r;
+      const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
+      smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
+      closest = other < shortest ? f.sc + k : closest;                  // :105
+      shortest = gmin(shortest, other);
+      const float nf = gclamp(other, 0.0f, 0.5f) * 2.0f;
+      snx = nf * snx - (1.0f - nf) * ox;
+      sny = nf * sny - (1.0f - nf) * oy;
+      snz = nf * snz - (1.0f - nf) * oz;
+    }
+    ball_dist += smooth + 0.01f;
+  }
+
+  // ---- wall or ball (:114-120) ----
+  const int wall = smooth < 0.01f ? 0 : 1;
+  const float cw = (float)wall, cb = (float)(1 - wall);
+  total = cw * total + cb * ball_dist;
+  draw = wall ? draw : closest;
+  px = cw * px + cb * (cx + dx * ball_dist);
+  py = cw * py + cb * (cy + dy * ball_dist);
+  pz = cw * pz + cb * (cz + dz * ball_dist);
+  const float nsign = cw * -1.0f + cb;
+
+  // ---- texture (:123-126) ----
+  const GlslMat& m = f.mats[draw];
+  const float rpx = snx * (1.0f - cw) + cw * (px - m.cx);
+  const float rpy = sny * (1.0f - cw) + cw * (py - m.cy);
+  const float rpz = snz * (1.0f - cw) + cw * (pz - m.cz);
+  const float uv0 = m.uv[0];
+  const float ycoord = gmod(rpy / (0.8f + 0.2f * (fabsf(rpx) + fabsf(rpz))), uv0) + m.uv[3];
+  const float xcoord = gmod(gmin(fabsf(rpz), fabsf(rpx)), uv0) + m.uv[2];
+  const float lod = total * 0.05f;
+  float cr, cg, cbl;
+  const int q = f.mip_levels - 1;
+  if (!(lod > 0.0f)) {
+    texel(f, 0, xcoord, ycoord, cr, cg, cbl);
+  } else if (lod >= (float)q) {
+    texel(f, q, xcoord, ycoord, cr, cg, cbl);
+  } else {
+    const float fl = floorf(lod);
+    const int d1 = (int)fl;
+    const float fr = lod - fl;
+    float r1, g1, b1, r2, g2, b2;
+    texel(f, d1, xcoord, ycoord, r1, g1, b1);
+    texel(f, d1 + 1, xcoord, ycoord, r2, g2, b2);
+    cr = (1.0f - fr) * r1 + fr * r2;
+    cg = (1.0f - fr) * g1 + fr * g2;
+    cbl = (1.0f - fr) * b1 + fr * b2;
+  }
+
+  // ---- lighting (:128-151) ----
+  float bright = 1.0f / gmax(total, 1.0f);
+  const float lightc = ((float)draw < (float)f.sc ? 0.0f : 1.0f) *
+                       ((float)(f.sc + f.lc - 1) < (float)draw ? 0.0f : 1.0f);
+  const int nshadow = f.all - f.sc - f.lc;
+  for (int li = 0; li < f.lc; li++) {
+    const GlslBall L = f.balls[li];
+    const float tlx = L.x - px, tly = L.y - py, tlz = L.z - pz;
+    const float tll = len3(tlx, tly, tlz);
+    const float tnx = tlx / tll, tny = tly / tll, tnz = tlz / tll;
+    const float vx = rpx * nsign, vy = rpy * nsign, vz = rpz * nsign;
+    const float vl = len3(vx, vy, vz);
+    const float nm = len3(vx / vl + tnx, vy / vl + tny, vz / vl + tnz) - 1.0f;
+    float shadow = 1.0f;
+    if (draw < f.sc + f.lc) {             // `drawSphere < j` holds for every j >= sc + lc
+      const float t = gclamp((nm - 0.0f) / (0.5f - 0.0f), 0.0f, 1.0f);
+      const float smooth_nm = t * t * (3.0f - 2.0f * t);                 // smoothstep(0, .5, nm)
+      for (int k = 0; k < nshadow; k++) {
+        const GlslPair P = f.pairs[li * nshadow + k];
+        float sangle = sfrt_math::acosf((-tnx * P.ux + -tny * P.uy) + -tnz * P.uz);
+        const float psd = 1.5f / (0.8f + 0.2f * len3(px - P.bx, py - P.by, pz - P.bz));
+        sangle = sangle * psd - (psd - 1.0f) * P.sanglet;
+        const float st = tll < P.dist ? 0.0f : 1.0f;                      // step(dist, tll)
+        shadow *= gclamp(sangle / P.sanglet + 1.0f - st * smooth_nm, 0.0f, 1.0f);
+      }
+    }
+    bright += 10.0f / tll / tll * gmax(0.5f + 0.5f * nm, 0.0f) * shadow;
+  }
+
+  // ---- colour (:153-158) ----
+  bright = lightc * 2.0f + (1.0f - lightc) * bright;
+  const float la = m.light[3];
+  cr = la * m.light[0] * 0.5f + (1.0f - la) * cr;
+  cg = la * m.light[1] * 0.5f + (1.0f - la) * cg;
+  cbl = la * m.light[2] * 0.5f + (1.0f - la) * cbl;
+  const float viewDist = 50.0f;
+  const float fog = gclamp(bright, 0.0f, 3.0f) + gmin(-total + viewDist * 0.66f, 0.0f);
+  cr *= fog;
+  cg *= fog;
+  cbl *= fog;
+  f.out[(long long)(row - f.row0) * f.out_pitch + i] =
+      unorm8(cr) | (unorm8(cg) << 8) | (unorm8(cbl) << 16) | (255u << 24);
+}
+
+__global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tx = tile % f.tiles_x, ty = tile / f.tiles_x;
+  const int i = tx * 8 + (lane & 7);
+  const int r = ty * 8 + (lane >> 3);
+  if (i >= f.width || r >= f.rows) return;
+  fragment(f, i, f.row0 + r);
+}
+
+}  // namespace
+
+int launch_glsl(const GlslFrame& f, void* stream) {
+  const int tiles_y = (f.rows + 7) / 8;
+  const long long tiles = (long long)f.tiles_x * tiles_y;
+  if (tiles == 0) return 0;
+  const dim3 g((unsigned)((tiles + 3) / 4)), b(256);
+  hipLaunchKernelGGL(k_glsl, g, b, 0, (hipStream_t)stream, f);
+  return hipGetLastError() != hipSuccess;
+}
+
+}  // namespace sfrt

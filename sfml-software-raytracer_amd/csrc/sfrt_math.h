@@ -172,4 +172,47 @@ SFRT_HD float asinf(float x) {
   return (int32_t)hx > 0 ? r : -r;
 }
 
+// e_acosf.c (glibc's __ieee754_acosf, the `acos` of the GLSL restatement,
+// rayShader.frag:142).
+SFRT_HD float acosf(float x) {
+  const float pi = u2f(0x40490fdau);
+  const float pio2_hi = u2f(0x3fc90fdau);
+  const float pio2_lo = u2f(0x33a22168u);
+  const float pS0 = u2f(0x3e2aaaabu), pS1 = u2f(0xbea6b090u), pS2 = u2f(0x3e4e0aa8u),
+              pS3 = u2f(0xbd241146u), pS4 = u2f(0x3a4f7f04u), pS5 = u2f(0x3811ef08u);
+  const float qS1 = u2f(0xc019d139u), qS2 = u2f(0x4001572du), qS3 = u2f(0xbf303361u),
+              qS4 = u2f(0x3d9dc62eu);
+  const uint32_t hx = f2u(x);
+  const uint32_t ix = hx & 0x7fffffffu;
+  if (ix == 0x3f800000u)                                   // |x| == 1
+    return (int32_t)hx > 0 ? 0.0f : pi + u2f(0x34222168u);  // pi + 2*pio2_lo
+  if (ix > 0x3f800000u) return (x - x) / (x - x);          // |x| > 1: NaN
+  if (ix < 0x3f000000u) {                                  // |x| < 0.5
+    if (ix <= 0x32800000u) return pio2_hi + pio2_lo;       // |x| <= 2^-26
+    const float z = x * x;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  }
+  if ((int32_t)hx < 0) {                                   // x < -0.5
+    const float z = (1.0f + x) * 0.5f;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float s = __builtin_sqrtf(z);
+    const float r = p / q;
+    const float w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  }
+  const float z = (1.0f - x) * 0.5f;                       // x > 0.5
+  const float s = __builtin_sqrtf(z);
+  const float df = u2f(f2u(s) & 0xfffff000u);
+  const float c = (z - df * df) / (s + df);
+  const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  const float r = p / q;
+  const float w = r * s + c;
+  return 2.0f * (df + w);
+}
+
 }  // namespace sfrt_math

@@ -40,6 +40,9 @@ ABI_SYMBOLS = (
     "sfrt_voxel_load_dyn_texture", "sfrt_voxel_set_colors", "sfrt_voxel_set_dynamics",
     "sfrt_voxel_set_lights", "sfrt_voxel_update_image", "sfrt_voxel_render_band",
     "sfrt_voxel_check",
+    "sfrt_glsl_create", "sfrt_glsl_destroy", "sfrt_glsl_set_ground", "sfrt_glsl_set_uniforms",
+    "sfrt_glsl_get_uniforms", "sfrt_glsl_set_uniform", "sfrt_glsl_set_uniform_int",
+    "sfrt_glsl_draw", "sfrt_glsl_draw_image", "sfrt_glsl_check",
 )
 
 
@@ -128,6 +131,16 @@ def lib() -> ctypes.CDLL:
         "sfrt_voxel_update_image": ([vp, vp, c_int, c_int, c_int, c_int], c_int),
         "sfrt_voxel_render_band": ([vp, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
         "sfrt_voxel_check": ([vp, vp], c_int),
+        "sfrt_glsl_create": ([c_int, P(vp)], c_int),
+        "sfrt_glsl_destroy": ([vp], None),
+        "sfrt_glsl_set_ground": ([vp, vp, c_int, c_int], c_int),
+        "sfrt_glsl_set_uniforms": ([vp, vp], c_int),
+        "sfrt_glsl_get_uniforms": ([vp, vp], c_int),
+        "sfrt_glsl_set_uniform": ([vp, ctypes.c_char_p, vp, c_int], c_int),
+        "sfrt_glsl_set_uniform_int": ([vp, ctypes.c_char_p, c_int], c_int),
+        "sfrt_glsl_draw": ([vp, vp, c_int, c_int, ctypes.c_int64, c_int, c_int, vp], c_int),
+        "sfrt_glsl_draw_image": ([vp, vp, c_int, c_int], c_int),
+        "sfrt_glsl_check": ([vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -400,3 +413,70 @@ class VoxelWorld:
 
     def check(self, stream: int = 0) -> None:
         _check(lib().sfrt_voxel_check(self._h, ctypes.c_void_p(stream or None)), "voxel_check")
+
+
+class GlslShader:
+    """Device-backed rayShader.frag: the uniform state of
+    ``SphereWorld::shader`` plus ``rt.draw(sp, &shader)``.  Uniform blocks are
+    glsl_scenes.UNIFORM_DTYPE records (the layout of sfrt_glsl_uniforms)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().sfrt_glsl_create(int(device), ctypes.byref(h)), "sfrt_glsl_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().sfrt_glsl_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_ground(self, rgba, w: int, h: int) -> None:
+        buf = np.ascontiguousarray(rgba, dtype=np.uint8)
+        if buf.size != w * h * 4:
+            raise ValueError("ground size mismatch")
+        _check(lib().sfrt_glsl_set_ground(self._h, buf.ctypes.data, int(w), int(h)), "set_ground")
+
+    def set_uniforms(self, u) -> None:
+        rec = np.ascontiguousarray(np.asarray(u).reshape(()))
+        _check(lib().sfrt_glsl_set_uniforms(self._h, rec.ctypes.data), "set_uniforms")
+
+    def get_uniforms(self, dtype):
+        rec = np.zeros((), dtype=dtype)
+        _check(lib().sfrt_glsl_get_uniforms(self._h, rec.ctypes.data), "get_uniforms")
+        return rec
+
+    def set_uniform(self, name: str, value) -> None:
+        """sf::Shader::setUniform: floats/vectors by name, ints for the counts."""
+        if isinstance(value, (int, np.integer)):
+            _check(lib().sfrt_glsl_set_uniform_int(self._h, name.encode(), int(value)), name)
+            return
+        v = np.ascontiguousarray(np.atleast_1d(np.asarray(value, dtype=np.float32)))
+        _check(lib().sfrt_glsl_set_uniform(self._h, name.encode(), v.ctypes.data, v.size), name)
+
+    def draw(self, dev_ptr: int, width: int, height: int, pitch_bytes: int, row0: int = 0,
+             rows: int | None = None, stream: int = 0) -> None:
+        rows = height - row0 if rows is None else rows
+        _check(lib().sfrt_glsl_draw(self._h, ctypes.c_void_p(dev_ptr), int(width), int(height),
+                                    int(pitch_bytes), int(row0), int(rows),
+                                    ctypes.c_void_p(stream or None)), "glsl_draw")
+
+    def draw_image(self, width: int, height: int) -> np.ndarray:
+        out = np.zeros(width * height * 4, dtype=np.uint8)
+        _check(lib().sfrt_glsl_draw_image(self._h, out.ctypes.data, int(width), int(height)),
+               "glsl_draw_image")
+        return out
+
+    def check(self, stream: int = 0) -> None:
+        _check(lib().sfrt_glsl_check(self._h, ctypes.c_void_p(stream or None)), "glsl_check")

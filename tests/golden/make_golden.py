@@ -1,6 +1,6 @@
 """Generate tests/golden/ from the CPU restatement (oracle/).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--only-glsl]
 
 Writes golden.json: per (config, pose) the frame's FNV-1a-64 and SHA-256,
 per-row FNV-1a-64 for frames up to 4K, the march-iteration statistics, and
@@ -40,8 +40,28 @@ def iteration_stats(o, width, height):
             "max": int(it.max())}
 
 
+def glsl_section(threads):
+    """GLSL renderer, oracle/glsl_oracle.c."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_glsl import GLSL_CASES
+    floor = scenes.load_floor()
+    sec = {}
+    for key, w, h, make in GLSL_CASES:
+        frame = oracle.GlslOracle(make(w, h), *floor).render(w, h, threads)
+        sec[key] = {"width": w, "height": h, "fnv1a64": oracle.fnv1a64(frame)}
+        print("glsl", key, sec[key]["fnv1a64"], flush=True)
+    return sec
+
+
 def main():
     oracle.build()
+    if "--only-glsl" in sys.argv:
+        path = os.path.join(HERE, "golden.json")
+        out = json.load(open(path))
+        out["glsl"] = glsl_section(os.cpu_count() or 1)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=0, sort_keys=True)
+        return
     tex, tw, th = scenes.load_floor()
     threads = os.cpu_count() or 1
     out = {"generator": "tests/golden/make_golden.py (oracle/sphereworld_oracle.c)",
@@ -85,6 +105,7 @@ def main():
                                         "rotation": r, "hrotation": hr,
                                         "fnv1a64": oracle.fnv1a64(frame)}
         print("voxel", case_key(case), out["voxel"][case_key(case)]["fnv1a64"], flush=True)
+    out["glsl"] = glsl_section(threads)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=0, sort_keys=True)
 

@@ -1,7 +1,7 @@
-// Host check of sfrt_math.h against the host libm (glibc 2.35 atanf/atan2f/asinf).
+// Host check of sfrt_math.h against the host libm (glibc 2.35 atanf/atan2f/asinf/acosf).
 // Built and run by tests/test_math_exhaustive.py:
 //   g++ -O2 -std=c++17 -ffp-contract=off -fopenmp math_check.cpp -o math_check
-//   ./math_check asinf|atanf            -> every binary32 input
+//   ./math_check asinf|atanf|acosf      -> every binary32 input
 //   ./math_check atan2f <npairs> <seed> -> random + structured pairs
 //   ./math_check atan2f_x1 | atan2f_y1  -> atan2f(y, 1) / atan2f(1, x) for every binary32
 //   ./math_check divpi                  -> q/PI2 + 1 and q/PI + 0.5 for every finite q
@@ -26,14 +26,15 @@ int main(int argc, char** argv) {
   if (argc < 2) return 2;
   const char* fn = argv[1];
   unsigned long long bad = 0, checked = 0;
-  if (!strcmp(fn, "asinf") || !strcmp(fn, "atanf")) {
-    const bool is_asin = !strcmp(fn, "asinf");
+  if (!strcmp(fn, "asinf") || !strcmp(fn, "atanf") || !strcmp(fn, "acosf")) {
+    const int which = !strcmp(fn, "asinf") ? 0 : !strcmp(fn, "atanf") ? 1 : 2;
 #pragma omp parallel for reduction(+ : bad, checked) schedule(static)
     for (long long hi = 0; hi < 65536; hi++) {
       for (uint32_t lo = 0; lo < 65536; lo++) {
         const float x = fl((uint32_t)(hi << 16) | lo);
-        const float want = is_asin ? ::asinf(x) : ::atanf(x);
-        const float got = is_asin ? sfrt_math::asinf(x) : sfrt_math::atanf(x);
+        const float want = which == 0 ? ::asinf(x) : which == 1 ? ::atanf(x) : ::acosf(x);
+        const float got = which == 0 ? sfrt_math::asinf(x)
+                          : which == 1 ? sfrt_math::atanf(x) : sfrt_math::acosf(x);
         checked++;
         if (!same(want, got)) {
           if (bad < 5) {

@@ -1,7 +1,7 @@
 // Device check of sfrt_math.h on gfx950 against the host libm (glibc 2.35).
 // Built and run by tests/test_gpu_parity.py::test_device_math_matches_libm:
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fopenmp math_gpu_check.hip
-//   ./math_gpu_check asinf|atanf [stride]   -> every stride-th binary32 pattern
+//   ./math_gpu_check asinf|atanf|acosf [stride] -> every stride-th binary32 pattern
 //   ./math_gpu_check atan2f <npairs>        -> random + scene-range pairs
 //   ./math_gpu_check sqrt_div [stride]      -> correctly rounded sqrtf and x/y vs the host
 //   ./math_gpu_check divpi                  -> x/PI2 + 1 and x/PI + 0.5 (fma form) for every finite x
@@ -33,6 +33,7 @@ __global__ void k_eval(int fn, const float* __restrict__ x, const float* __restr
     case 4: r = x[i] / y[i]; break;
     case 5: r = sfrt_math::div_pi2_plus_1(x[i]); break;
     case 6: r = sfrt_math::div_pi_plus_half(x[i]); break;
+    case 8: r = sfrt_math::acosf(x[i]); break;
     default: r = sfrt_math::atan2f(x[i], 1.0f); break;
   }
   out[i] = r;
@@ -47,6 +48,7 @@ static float host_eval(int fn, float x, float y) {
     case 4: return x / y;
     case 5: return std::isfinite(x) ? x / 6.28318530718f + 1.0f : NAN;
     case 6: return std::isfinite(x) ? x / 3.1415926535f + 0.5f : NAN;
+    case 8: return ::acosf(x);
     default: return ::atan2f(x, 1.0f);
   }
 }
@@ -69,6 +71,7 @@ int main(int argc, char** argv) {
   else if (!strcmp(argv[1], "sqrt_div")) fn = 3;
   else if (!strcmp(argv[1], "divpi")) fn = 5;
   else if (!strcmp(argv[1], "atan2f_x1")) fn = 7;
+  else if (!strcmp(argv[1], "acosf")) fn = 8;
   else return 2;
   const long long total = fn == 2 ? (argc > 2 ? atoll(argv[2]) : 100000000LL)
                                   : (4294967296LL / (argc > 2 ? atoll(argv[2]) : 1));

@@ -1,0 +1,267 @@
+"""GLSL renderer: rayShader.frag run per render-target pixel,
+/root/reference/Raytracing/rayShader.frag:1-179, uniforms from
+SphereWorld.cpp:214-238 and Source.cpp:143-146.
+
+CPU: the uniform replay (glsl_scenes.py) reproduces the survey's srand(0)
+scene; the restatement (oracle/glsl_oracle.c) is deterministic across threads
+and bands and matches its committed golden hashes (tests/golden/golden.json
+"glsl").  GPU: libsfrt.so's GLSL kernel equals the restatement byte for byte.
+Parity against the reference's own OpenGL output is unpinned (no GL context
+can run here; DESIGN.md 4b fixes the semantics the shader leaves open).
+"""
+import ctypes
+import ctypes.util
+import json
+import os
+
+import numpy as np
+import pytest
+
+import glsl_scenes as gs
+import oracle
+import scenes
+from conftest import ROOT, host_threads
+
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+
+# (key, width, height, uniform builder)
+GLSL_CASES = [
+    ("default@320x180", 320, 180, lambda w, h: gs.default_uniforms(w, h)),
+    ("default@1920x1080", 1920, 1080, lambda w, h: gs.default_uniforms(w, h)),
+    ("default@1920x1080/0.7,0.3", 1920, 1080, lambda w, h: gs.default_uniforms(w, h, 0.7, 0.3)),
+    ("frames300@1920x1080/5.5,-0.4", 1920, 1080,
+     lambda w, h: gs.default_uniforms(w, h, 5.5, -0.4, frames=300)),
+    ("default@3840x2160/2.5,-0.2", 3840, 2160, lambda w, h: gs.default_uniforms(w, h, 2.5, -0.2)),
+    ("random1(1,0,0)@320x180", 320, 180, lambda w, h: gs.random_uniforms(1, 1, 0, 0, w, h)),
+    ("random2(12,2,14)@320x180", 320, 180, lambda w, h: gs.random_uniforms(2, 12, 2, 14, w, h)),
+    ("random3(40,4,50)@640x360", 640, 360, lambda w, h: gs.random_uniforms(3, 40, 4, 50, w, h)),
+    ("random4(5,0,9)@333x97", 333, 97, lambda w, h: gs.random_uniforms(4, 5, 0, 9, w, h)),
+]
+CPU_CASES = [c for c in GLSL_CASES if c[1] * c[2] <= 640 * 360]
+
+
+def synthetic_ground(w=64, h=32, seed=5):
+    return np.random.default_rng(seed).integers(0, 256, w * h * 4, dtype=np.uint8), w, h
+
+
+@pytest.fixture(scope="module")
+def floor():
+    return scenes.load_floor()
+
+
+def glsl_oracle(case, floor):
+    _, w, h, make = case
+    return oracle.GlslOracle(make(w, h), *floor)
+
+
+# ---------------- CPU ----------------
+
+def test_constructor_replay_reproduces_default10():
+    """srand(0) + the constructor's rand() order gives the survey's default10
+    walls -- pins the uniform fixture."""
+    w = gs.ShaderWorld(0)
+    walls = np.array([(*b.pos, b.radius) for b in w.spheres], np.float32)
+    assert np.array_equal(walls, scenes.default10().spheres)
+    u = w.uniforms()
+    assert (int(u["sphere_count"]), int(u["light_count"]), int(u["all_spheres_count"])) == (10, 1, 21)
+    # history: the light's uvs slot keeps osphere 0's value from before AddLight
+    assert u["uvs"][10].tolist() == [0.5, 1.0, 0.5, 0.0]
+    assert u["lights"][10].tolist() == [1.0, 1.0, 1.0, 1.0]
+    assert np.all(u["lights"][11:21] == np.float32([0.5, 1, 1, 1]))
+    assert set(u["spheres"][11:21, 3].tolist()) == {float(np.float32(0.3)), float(np.float32(0.6))}
+
+
+def test_glibc_rand_emulation():
+    libc = ctypes.CDLL(ctypes.util.find_library("c"))
+    for seed in (0, 1, 42, 2**31 - 1):
+        libc.srand(seed)
+        r = gs.GlibcRand(seed)
+        assert [libc.rand() for _ in range(500)] == [r() for _ in range(500)]
+
+
+def test_update_world_moves_ospheres_only():
+    w = gs.ShaderWorld(0)
+    before = w.uniforms()
+    for _ in range(50):
+        w.update_world()
+    after = w.uniforms()
+    assert np.array_equal(before["spheres"][:11], after["spheres"][:11])
+    assert not np.array_equal(before["spheres"][11:21], after["spheres"][11:21])
+
+
+@pytest.mark.parametrize("case", CPU_CASES, ids=[c[0] for c in CPU_CASES])
+def test_oracle_matches_golden(case, floor):
+    o = glsl_oracle(case, floor)
+    frame = o.render(case[1], case[2], host_threads())
+    assert oracle.fnv1a64(frame) == GOLDEN["glsl"][case[0]]["fnv1a64"]
+
+
+def test_oracle_threads_and_bands_agree(floor):
+    case = GLSL_CASES[6]
+    o = glsl_oracle(case, floor)
+    w, h = case[1], case[2]
+    full = o.render(w, h, 1)
+    assert np.array_equal(full, o.render(w, h, 7))
+    parts = [o.render_band(w, h, r0, min(37, h - r0)) for r0 in range(0, h, 37)]
+    assert np.array_equal(full, np.concatenate(parts))
+
+
+def test_oracle_known_answers(floor):
+    """Spot values the shader's formulas fix exactly (rayShader.frag:153-158)."""
+    u = gs.default_uniforms(320, 180)
+    o = oracle.GlslOracle(u, *floor)
+    frame = o.render(320, 180, host_threads()).reshape(180, 320, 4)
+    assert (frame[..., 3] == 255).all()
+    seen = set()
+    for row in range(0, 180, 6):
+        for i in range(0, 320, 6):
+            d = o.pixel(320, 180, i, row)
+            ds = d["draw_sphere"]
+            assert 0 <= ds < 21
+            if d["checkstep"] == 0 and ds == 10:       # the light: 0.5 * rgb * (2 + fog)
+                assert frame[row, i, :3].tolist() == [255, 255, 255]
+                seen.add("light")
+            if d["checkstep"] == 1:
+                assert ds < 10 and d["total_dist"] == d["wall_dist"]
+                seen.add("wall")
+            if d["checkstep"] == 0 and ds > 10:
+                seen.add("ball")
+    assert seen == {"light", "wall", "ball"}
+
+
+def test_march_steps_are_bounded(floor):
+    o = oracle.GlslOracle(gs.default_uniforms(320, 180), *floor)
+    steps = o.march_steps(320, 180, host_threads())
+    assert steps.min() >= 1 and steps.max() < 100
+
+
+# ---------------- GPU ----------------
+
+@pytest.fixture(scope="module")
+def shader(built, floor):
+    import sfrt
+    s = sfrt.GlslShader(0)
+    s.set_ground(*floor)
+    return s
+
+
+def draw(shader, u, w, h):
+    shader.set_uniforms(u)
+    return shader.draw_image(w, h)
+
+
+def first_diff(got, want, w):
+    bad = np.nonzero(np.any(got.reshape(-1, 4) != want.reshape(-1, 4), axis=1))[0]
+    if bad.size == 0:
+        return ""
+    k = int(bad[0])
+    return f"{bad.size} pixels differ, first ({k % w}, {k // w}): {got.reshape(-1, 4)[k]} vs " \
+           f"{want.reshape(-1, 4)[k]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", GLSL_CASES, ids=[c[0] for c in GLSL_CASES])
+def test_gpu_matches_oracle(shader, floor, case):
+    key, w, h, make = case
+    u = make(w, h)
+    got = draw(shader, u, w, h)
+    want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+    assert np.array_equal(got, want), first_diff(got, want, w)
+    assert oracle.fnv1a64(got) == GOLDEN["glsl"][key]["fnv1a64"]
+
+
+@pytest.mark.gpu
+def test_gpu_synthetic_ground_mips(shader, floor):
+    """Non-square ground (64x32: 2x1 box levels) over the default uniforms."""
+    import sfrt
+    g = synthetic_ground()
+    s = sfrt.GlslShader(0)
+    s.set_ground(*g)
+    for w, h, rot in [(320, 180, (0.0, 0.0)), (400, 300, (1.9, 0.45))]:
+        u = gs.default_uniforms(w, h, *rot, frames=120)
+        got = draw(s, u, w, h)
+        want = oracle.GlslOracle(u, *g).render(w, h, host_threads())
+        assert np.array_equal(got, want), first_diff(got, want, w)
+    s.close()
+
+
+@pytest.mark.gpu
+def test_gpu_bands_tile_the_frame(shader, floor):
+    import torch
+    w, h = 1920, 1080
+    u = gs.default_uniforms(w, h, 0.3, 0.1, frames=40)
+    shader.set_uniforms(u)
+    full = shader.draw_image(w, h)
+    buf = torch.zeros(h, w * 4 + 64, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    for r0 in range(0, h, 250):
+        rows = min(250, h - r0)
+        shader.draw(buf[r0].data_ptr(), w, h, buf.stride(0), r0, rows, stream.cuda_stream)
+    stream.synchronize()
+    shader.check(stream.cuda_stream)
+    got = buf[:, : w * 4].cpu().numpy().ravel()
+    assert np.array_equal(got, full)
+
+
+@pytest.mark.gpu
+def test_gpu_set_uniform_by_name_replay(built, floor):
+    """UpdateSpheres + main()'s setUniform calls by name give the same frame as
+    the uniform block (SphereWorld.cpp:214-238, Source.cpp:143-146)."""
+    import sfrt
+    w, h = 480, 270
+    u = gs.default_uniforms(w, h, 1.2, 0.2, frames=10)
+    s = sfrt.GlslShader(0)
+    s.set_ground(*floor)
+    n = int(u["all_spheres_count"])
+    for k in range(n):
+        s.set_uniform(f"spheres[{k}]", u["spheres"][k])
+        s.set_uniform(f"lights[{k}]", u["lights"][k])
+        s.set_uniform(f"uvs[{k}]", u["uvs"][k])
+    s.set_uniform("lightCount", int(u["light_count"]))
+    s.set_uniform("sphereCount", int(u["sphere_count"]))
+    s.set_uniform("allSpheresCount", int(u["all_spheres_count"]))
+    for name in ("campos", "rotation", "fov", "size"):
+        s.set_uniform(name, u[name])
+    got = s.draw_image(w, h)
+    want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+    assert np.array_equal(got, want), first_diff(got, want, w)
+    back = s.get_uniforms(gs.UNIFORM_DTYPE)
+    assert back.tobytes() == np.asarray(u).tobytes()
+    with pytest.raises(sfrt.SfrtError):
+        s.set_uniform("spheres[100]", [0, 0, 0, 1])
+    with pytest.raises(sfrt.SfrtError):
+        s.set_uniform("nosuch", [1.0, 2.0])
+    with pytest.raises(sfrt.SfrtError):
+        s.set_uniform("campos", [1.0, 2.0])
+    s.close()
+
+
+@pytest.mark.gpu
+def test_gpu_errors_fail_loudly(built, floor):
+    import sfrt
+    s = sfrt.GlslShader(0)
+    u = gs.default_uniforms(64, 64)
+    s.set_uniforms(u)
+    with pytest.raises(sfrt.SfrtError, match="NO_TEXTURE"):
+        s.draw_image(64, 64)
+    with pytest.raises(sfrt.SfrtError, match="INVALID"):
+        s.set_ground(np.zeros(48 * 32 * 4, np.uint8), 48, 32)
+    s.set_ground(*floor)
+    bad = u.copy()
+    bad["spheres"][3][1] = np.nan
+    s.set_uniforms(bad)
+    with pytest.raises(sfrt.SfrtError, match="INVALID"):
+        s.draw_image(64, 64)
+    bad = u.copy()
+    bad["all_spheres_count"] = 101
+    s.set_uniforms(bad)
+    with pytest.raises(sfrt.SfrtError, match="INVALID"):
+        s.draw_image(64, 64)
+    bad = u.copy()
+    bad["size"] = (0.0, 64.0)
+    s.set_uniforms(bad)
+    with pytest.raises(sfrt.SfrtError, match="INVALID"):
+        s.draw_image(64, 64)
+    s.set_uniforms(u)
+    assert s.draw_image(64, 64).size == 64 * 64 * 4
+    s.close()

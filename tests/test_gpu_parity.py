@@ -192,7 +192,8 @@ def test_errors_fail_loudly(world):
 
 
 @pytest.mark.parametrize("fn,arg", [("asinf", "1"), ("atanf", "1"), ("atan2f", "100000000"),
-                                    ("sqrt_div", "16"), ("divpi", "1"), ("atan2f_x1", "1")])
+                                    ("sqrt_div", "16"), ("divpi", "1"), ("atan2f_x1", "1"),
+                                    ("acosf", "1")])
 def test_device_math_matches_libm(fn, arg, tmp_path):
     """sfrt_math on gfx950 vs host glibc: every binary32 input (atanf, asinf)."""
     exe = tmp_path / "math_gpu_check"

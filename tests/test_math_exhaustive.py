@@ -1,8 +1,8 @@
-"""sfrt_math.h (the kernels' atanf / atan2f / asinf) == host libm, bit for bit.
+"""sfrt_math.h (the kernels' atanf / atan2f / asinf / acosf) == host libm, bit for bit.
 
 Host build of the same header the kernel uses, compiled with
 -ffp-contract=off, checked against glibc 2.35 over every binary32 input of
-asinf and atanf (2^32 each) and 10^8 atan2f pairs (random bit patterns and
+asinf, atanf and acosf (2^32 each) and 10^8 atan2f pairs (random bit patterns and
 the |coord| < 64 range hit points live in).  The gfx950 build of the header
 is checked the same way in test_gpu_parity.py::test_device_math_matches_libm.
 """
@@ -23,7 +23,7 @@ def math_check(tmp_path_factory):
     return str(exe)
 
 
-@pytest.mark.parametrize("args", [["asinf"], ["atanf"], ["atan2f", "100000000", "1"],
+@pytest.mark.parametrize("args", [["asinf"], ["atanf"], ["acosf"], ["atan2f", "100000000", "1"],
                                   ["atan2f_x1"], ["atan2f_y1"], ["divpi"]])
 def test_restated_math_matches_libm(math_check, args):
     r = subprocess.run([math_check] + args, capture_output=True, text=True, timeout=900)
