@@ -28,6 +28,8 @@ struct GlslWall {                      // spheres[0 .. sphereCount)
 
 struct GlslBall {                      // spheres[sphereCount .. allSpheresCount)
   float x, y, z, r;
+  float r_skip;                        // r when r >= 0 (the march's dominance test), else NaN
+  float pad0, pad1, pad2;
 };
 
 struct GlslPair {                      // light i, shadow ball j (:140-142)
@@ -35,6 +37,7 @@ struct GlslPair {                      // light i, shadow ball j (:140-142)
   float sanglet;                       // atan(spheres[j].w, dist)
   float ux, uy, uz;                    // (spheres[j] - spheres[i]) / dist
   float bx, by, bz;                    // spheres[j].xyz
+  float cos_lit;                       // dot(-tolightnorm, u) <= cos_lit => factor 1 (or -2)
 };
 
 struct GlslMat {                       // per uniform index: uvs[k], lights[k], spheres[k].xyz
@@ -48,6 +51,7 @@ struct GlslFrame {
   float fwd[3], right[3], up[3];
   float fov_x, fov_y, hk, vk;          // hk = fov.x / size.x * 2 (:172), vk likewise
   int32_t sc, lc, all;
+  int32_t cam_negzero;                 // a campos component is -0.0 (wall pass, below)
   int32_t width, height, row0, rows, tiles_x;
   const GlslWall* walls;
   const GlslBall* balls;               // all - sc entries (lights, then ospheres)

@@ -75,18 +75,25 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
     const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
     const float s = (rx * rx + ry * ry) + rz * rz;
     const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
-    float tosurf = 0.0f;                               // the step-0 value: 0 * (...) * 0.5 == +0
     if (__builtin_amdgcn_ballot_w64(inside)) {
       const float cs = inside ? 1.0f : 0.0f;
       const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
       const float c = cs * s - w.rr;
-      tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
+      const float tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
+      px = px + dx * tosurf;
+      py = py + dy * tosurf;
+      pz = pz + dz * tosurf;
+      total = total + tosurf;
+    } else if (f.cam_negzero) {
+      // No lane inside: tosurf = 0 * (...) * 0.5 == +0 for every lane (the
+      // uniforms are bounded, so (...) is finite and >= 0).  pos + dir * +0
+      // then only turns a -0.0 component into +0.0, and pos holds a -0.0 only
+      // if campos does (x + y == -0 needs both -0); total + +0 == total.
+      px = px + dx * 0.0f;
+      py = py + dy * 0.0f;
+      pz = pz + dz * 0.0f;
     }
     draw = inside ? k : draw;
-    px = px + dx * tosurf;
-    py = py + dy * tosurf;
-    pz = pz + dz * tosurf;
-    total = total + tosurf;
     if (++k == f.sc) k = 0;
   }
 
@@ -110,7 +117,17 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
     for (int k = 0; k < nballs; k++) {
       const GlslBall b = f.balls[k];
       const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
-      const float other = len3(ox, oy, oz) - b.r;
+      const float ss = (ox * ox + oy * oy) + oz * oz;
+      // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
+      // margin), polsmin returns smooth, closest/shortest keep their values and
+      // normalFactor == 1, so the body changes nothing (smoothNormal at most
+      // flips the sign of a zero component, which no output depends on).
+      // Tested on the squared length with relative margins.
+      const float t = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f);
+      const float bnd = (b.r_skip + t * 1.00001f) + 1e-4f;
+      const bool dominated = ss >= bnd * bnd * 1.00001f;
+      if (!__builtin_amdgcn_ballot_w64(!dominated)) continue;
+      const float other = sqrt_cr(ss) - b.r;
       const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
       smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
       closest = other < shortest ? f.sc + k : closest;                  // :105
@@ -177,9 +194,14 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
     if (draw < f.sc + f.lc) {             // `drawSphere < j` holds for every j >= sc + lc
       const float t = gclamp((nm - 0.0f) / (0.5f - 0.0f), 0.0f, 1.0f);
       const float smooth_nm = t * t * (3.0f - 2.0f * t);                 // smoothstep(0, .5, nm)
+      const bool near = total < 1000.0f;
       for (int k = 0; k < nshadow; k++) {
         const GlslPair P = f.pairs[li * nshadow + k];
-        float sangle = sfrt_math::acosf((-tnx * P.ux + -tny * P.uy) + -tnz * P.uz);
+        const float cosang = (-tnx * P.ux + -tny * P.uy) + -tnz * P.uz;
+        // Ball outside the light cone seen from pos: acos(cosang) >= sanglet
+        // (with margin) makes the clamp's argument >= 1, factor 1 exactly.
+        if (!__builtin_amdgcn_ballot_w64(!(near && cosang <= P.cos_lit))) continue;
+        float sangle = sfrt_math::acosf(cosang);
         const float psd = 1.5f / (0.8f + 0.2f * len3(px - P.bx, py - P.by, pz - P.bz));
         sangle = sangle * psd - (psd - 1.0f) * P.sanglet;
         const float st = tll < P.dist ? 0.0f : 1.0f;                      // step(dist, tll)

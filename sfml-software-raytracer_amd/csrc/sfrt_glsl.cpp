@@ -200,6 +200,9 @@ struct sfrt_glsl {
     f.sc = sc;
     f.lc = lc;
     f.all = all;
+    f.cam_negzero = (std::signbit(v.campos[0]) && v.campos[0] == 0.0f) ||
+                    (std::signbit(v.campos[1]) && v.campos[1] == 0.0f) ||
+                    (std::signbit(v.campos[2]) && v.campos[2] == 0.0f);
     // tables
     const int nb = all - sc, ns = all - sc - lc;
     std::vector<sfrt::GlslWall> walls(sc > 0 ? sc : 1);
@@ -210,7 +213,7 @@ struct sfrt_glsl {
     std::vector<sfrt::GlslBall> balls(nb > 0 ? nb : 1);
     for (int k = 0; k < nb; k++) {
       const float* S = v.spheres[sc + k];
-      balls[k] = {S[0], S[1], S[2], S[3]};
+      balls[k] = {S[0], S[1], S[2], S[3], S[3] >= 0.0f ? S[3] : NAN, 0.0f, 0.0f, 0.0f};
     }
     std::vector<sfrt::GlslPair> pairs(lc * ns > 0 ? lc * ns : 1);
     for (int li = 0; li < lc; li++)
@@ -228,6 +231,12 @@ struct sfrt_glsl {
         P.bx = B[0];
         P.by = B[1];
         P.bz = B[2];
+        // acos(dot) >= sanglet * (1 + 1e-3) + 1e-3 suffices for a factor of 1
+        // (DESIGN.md 5c); only for balls near the camera (|pos - ball| < 2000).
+        const float cx = v.campos[0] - B[0], cy = v.campos[1] - B[1], cz = v.campos[2] - B[2];
+        const float dcam = std::sqrt((cx * cx + cy * cy) + cz * cz);
+        P.cos_lit = (P.sanglet > 0.0f && P.sanglet < 1.0f && dcam < 1000.0f)
+                        ? std::cos(P.sanglet * 1.001f + 1e-3f) : -2.0f;
       }
     std::vector<sfrt::GlslMat> mats(sfrt::kGlslMax);
     for (int k = 0; k < sfrt::kGlslMax; k++) {

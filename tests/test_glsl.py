@@ -185,6 +185,29 @@ def test_gpu_synthetic_ground_mips(shader, floor):
     s.close()
 
 
+def _negzero_cam(w, h):
+    u = gs.random_uniforms(6, 8, 2, 12, w, h)
+    u["campos"] = (-0.0, 0.25, -0.0)
+    return u
+
+
+def _far_balls(w, h):
+    """Balls far outside the walls: no dominance, long march, shadow pairs far away."""
+    u = gs.default_uniforms(w, h, 0.4, 0.2)
+    u["spheres"][11:21, :3] += np.float32(3000.0)
+    return u
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("make", [_negzero_cam, _far_balls], ids=["negzero_cam", "far_balls"])
+def test_gpu_edge_uniforms(shader, floor, make):
+    w, h = 320, 180
+    u = make(w, h)
+    got = draw(shader, u, w, h)
+    want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+    assert np.array_equal(got, want), first_diff(got, want, w)
+
+
 @pytest.mark.gpu
 def test_gpu_bands_tile_the_frame(shader, floor):
     import torch
