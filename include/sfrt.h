@@ -251,6 +251,16 @@ SFRT_API int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int heigh
 SFRT_API int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height);
 SFRT_API int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream);
 
+/* ======================================================================
+ * Asset pipeline: PNG -> RGBA8 as sf::Image::loadFromFile
+ * (SFML 2.4.2 / stb_image, 4 channels) decodes the reference's textures
+ * (SphereWorld.cpp:52-53, World.cpp:40-45).  Host-only; no device needed.
+ * ====================================================================== */
+SFRT_API int sfrt_png_info(const uint8_t* data, int64_t len, int* width, int* height);
+/* rgba: capacity bytes >= width*height*4 (query with sfrt_png_info). */
+SFRT_API int sfrt_png_decode(const uint8_t* data, int64_t len, uint8_t* rgba, int64_t capacity,
+                             int* width, int* height);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,7 @@ ABI_SYMBOLS = (
     "sfrt_glsl_create", "sfrt_glsl_destroy", "sfrt_glsl_set_ground", "sfrt_glsl_set_uniforms",
     "sfrt_glsl_get_uniforms", "sfrt_glsl_set_uniform", "sfrt_glsl_set_uniform_int",
     "sfrt_glsl_draw", "sfrt_glsl_draw_image", "sfrt_glsl_check",
+    "sfrt_png_info", "sfrt_png_decode",
 )
 
 
@@ -141,6 +142,8 @@ def lib() -> ctypes.CDLL:
         "sfrt_glsl_draw": ([vp, vp, c_int, c_int, ctypes.c_int64, c_int, c_int, vp], c_int),
         "sfrt_glsl_draw_image": ([vp, vp, c_int, c_int], c_int),
         "sfrt_glsl_check": ([vp, vp], c_int),
+        "sfrt_png_info": ([vp, ctypes.c_int64, P(c_int), P(c_int)], c_int),
+        "sfrt_png_decode": ([vp, ctypes.c_int64, vp, ctypes.c_int64, P(c_int), P(c_int)], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -413,6 +416,18 @@ class VoxelWorld:
 
     def check(self, stream: int = 0) -> None:
         _check(lib().sfrt_voxel_check(self._h, ctypes.c_void_p(stream or None)), "voxel_check")
+
+
+def decode_png(data: bytes) -> tuple[np.ndarray, int, int]:
+    """PNG bytes -> (RGBA8 uint8 array, width, height), as sf::Image::loadFromFile."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    w, h = ctypes.c_int(), ctypes.c_int()
+    _check(lib().sfrt_png_info(buf.ctypes.data, buf.size, ctypes.byref(w), ctypes.byref(h)),
+           "png_info")
+    out = np.empty(w.value * h.value * 4, dtype=np.uint8)
+    _check(lib().sfrt_png_decode(buf.ctypes.data, buf.size, out.ctypes.data, out.size,
+                                 ctypes.byref(w), ctypes.byref(h)), "png_decode")
+    return out, w.value, h.value
 
 
 class GlslShader:

@@ -1,0 +1,196 @@
+"""Asset pipeline: libsfrt.so's PNG decoder (sfrt_png_decode)
+reproduces sf::Image::loadFromFile -> stb_image's 4-channel output.
+
+PNGs written by the encoder below -- every colour type and bit depth, tRNS,
+Adam7, all five filters, split IDAT, ancillary chunks -- must decode to the
+pixels they were built from, expanded by stb_image's rules; a PIL-written
+PNG must decode like PIL reads it.  Host-only (no GPU).  The reference's own
+PNG files are not used (copying them in was refused).
+"""
+import io
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def sfrt(built):
+    import sfrt as mod
+    return mod
+
+
+def test_pil_written_png(sfrt):
+    from PIL import Image
+    rng = np.random.default_rng(7)
+    for mode, shape in [("RGBA", (37, 29, 4)), ("RGB", (16, 64, 3)), ("L", (9, 5))]:
+        img = Image.fromarray(rng.integers(0, 256, shape, dtype=np.uint8), mode)
+        buf = io.BytesIO()
+        img.save(buf, format="PNG")
+        rgba, w, h = sfrt.decode_png(buf.getvalue())
+        assert (w, h) == img.size
+        assert np.array_equal(rgba, np.asarray(img.convert("RGBA")).ravel())
+
+
+# ---------- a small PNG encoder for synthetic cases ----------
+
+ADAM7 = [(0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2),
+         (0, 1, 1, 2)]
+CHANNELS = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}
+
+
+def chunk(t, body):
+    return struct.pack(">I", len(body)) + t + body + struct.pack(">I", zlib.crc32(t + body))
+
+
+def pack_row(samples, depth):
+    if depth == 8:
+        return bytes(samples.astype(np.uint8))
+    if depth == 16:
+        return samples.astype(">u2").tobytes()
+    per = 8 // depth
+    out = bytearray((len(samples) + per - 1) // per)
+    for k, v in enumerate(samples):
+        out[k // per] |= int(v) << (8 - depth - (k % per) * depth)
+    return bytes(out)
+
+
+def paeth(a, b, c):
+    p = a + b - c
+    pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
+    return a if pa <= pb and pa <= pc else (b if pb <= pc else c)
+
+
+def filter_rows(rows, bpp, rng):
+    out = b""
+    prev = bytes(len(rows[0])) if rows else b""
+    for row in rows:
+        f = int(rng.integers(0, 5))
+        enc = bytearray(len(row))
+        for x in range(len(row)):
+            a = row[x - bpp] if x >= bpp else 0
+            b = prev[x]
+            c = prev[x - bpp] if x >= bpp else 0
+            pred = [0, a, b, (a + b) >> 1, paeth(a, b, c)][f]
+            enc[x] = (row[x] - pred) & 255
+        out += bytes([f]) + bytes(enc)
+        prev = row
+    return out
+
+
+def encode(img, color, depth, interlace=0, palette=None, trns=None, seed=0):
+    """img: (h, w, channels) integer samples at `depth`."""
+    h, w, ch = img.shape
+    rng = np.random.default_rng(seed)
+    bpp = max(1, ch * depth // 8)
+    passes = ADAM7 if interlace else [(0, 0, 1, 1)]
+    raw = b""
+    for x0, y0, dx, dy in passes:
+        sub = img[y0::dy, x0::dx]
+        if sub.shape[0] == 0 or sub.shape[1] == 0:
+            continue
+        rows = [pack_row(sub[y].reshape(-1), depth) for y in range(sub.shape[0])]
+        raw += filter_rows(rows, bpp, rng)
+    png = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, color, 0, 0,
+                                                              interlace))
+    png += chunk(b"gAMA", struct.pack(">I", 45455))        # ignored, like stb
+    if palette is not None:
+        png += chunk(b"PLTE", bytes(np.asarray(palette, np.uint8).ravel()))
+    if trns is not None:
+        png += chunk(b"tRNS", trns)
+    z = zlib.compress(raw, 9)
+    png += chunk(b"IDAT", z[: len(z) // 2]) + chunk(b"IDAT", z[len(z) // 2:])  # split IDAT
+    return png + chunk(b"IEND", b"")
+
+
+def stb_expect(img, color, depth, palette=None, pal_alpha=None, key=None):
+    """stb_image's 4-channel expansion of the samples (see sfrt_png.cpp)."""
+    h, w, ch = img.shape
+    scale = {1: 0xFF, 2: 0x55, 4: 0x11, 8: 1}
+    to8 = (lambda v: (v >> 8).astype(np.uint8)) if depth == 16 else \
+        (lambda v: (v * scale[depth]).astype(np.uint8))
+    out = np.zeros((h, w, 4), np.uint8)
+    if color == 3:
+        pal = np.zeros((256, 4), np.uint8)
+        pal[: len(palette), :3] = palette
+        pal[:, 3] = 255
+        if pal_alpha is not None:
+            pal[: len(pal_alpha), 3] = pal_alpha
+        pal[len(palette):, :3] = 0
+        return pal[img[..., 0]].ravel()
+    if color in (0, 4):
+        g = to8(img[..., 0])
+        out[..., 0] = out[..., 1] = out[..., 2] = g
+        if color == 4:
+            out[..., 3] = to8(img[..., 1])
+        elif key is None:
+            out[..., 3] = 255
+        elif depth == 16:
+            out[..., 3] = np.where(img[..., 0] == key, 0, 255)
+        else:
+            out[..., 3] = np.where(g == np.uint8(((key & 255) * scale[depth]) & 255), 0, 255)
+    else:
+        for c in range(3):
+            out[..., c] = to8(img[..., c])
+        if color == 6:
+            out[..., 3] = to8(img[..., 3])
+        elif key is None:
+            out[..., 3] = 255
+        else:
+            k = key if depth == 16 else [v & 255 for v in key]
+            m = (img[..., 0] == k[0]) & (img[..., 1] == k[1]) & (img[..., 2] == k[2])
+            out[..., 3] = np.where(m, 0, 255)
+    return out.ravel()
+
+
+CASES = []
+for color, depths in [(0, [1, 2, 4, 8, 16]), (2, [8, 16]), (3, [1, 2, 4, 8]), (4, [8, 16]),
+                      (6, [8, 16])]:
+    for depth in depths:
+        for interlace in (0, 1):
+            CASES.append((color, depth, interlace))
+
+
+@pytest.mark.parametrize("color,depth,interlace", CASES,
+                         ids=[f"c{c}_d{d}_i{i}" for c, d, i in CASES])
+def test_synthetic_png(sfrt, color, depth, interlace):
+    rng = np.random.default_rng(color * 100 + depth * 10 + interlace)
+    w, h = 13, 11
+    ch = CHANNELS[color]
+    top = (1 << depth) - 1
+    img = rng.integers(0, top + 1, (h, w, ch)).astype(np.int64)
+    palette = pal_alpha = key = trns = None
+    if color == 3:
+        n = min(256, top + 1) - 1 if depth < 8 else 200       # some indices past the palette
+        palette = rng.integers(0, 256, (max(1, n), 3))
+        pal_alpha = rng.integers(0, 256, max(1, n) // 2)
+        trns = bytes(pal_alpha.astype(np.uint8))
+        img = np.minimum(img, max(1, n) - 1) if depth == 8 else img
+    elif color == 0:
+        key = int(img[0, 0, 0])
+        trns = struct.pack(">H", key)
+    elif color == 2:
+        key = [int(v) for v in img[1, 2]]
+        trns = struct.pack(">HHH", *key)
+    data = encode(img, color, depth, interlace, palette, trns, seed=depth)
+    rgba, gw, gh = sfrt.decode_png(data)
+    assert (gw, gh) == (w, h)
+    want = stb_expect(img, color, depth, palette, pal_alpha, key)
+    assert np.array_equal(rgba, want)
+
+
+def test_malformed(sfrt):
+    img = np.arange(12, dtype=np.int64).reshape(2, 2, 3)
+    good = encode(img, 2, 8)
+    assert sfrt.decode_png(good)[1:] == (2, 2)
+    for bad in (good[:30], b"\x89PNX" + good[4:], good[:-20],
+                good[:8] + chunk(b"ABCD", b"xx") + good[8:]):
+        with pytest.raises(sfrt.SfrtError):
+            sfrt.decode_png(bad)
+    # CRCs are not checked (stb_image does not either)
+    pos = good.index(b"IDAT") - 4
+    n = struct.unpack(">I", good[pos:pos + 4])[0]
+    crc_at = pos + 8 + n
+    flipped = good[:crc_at] + bytes([good[crc_at] ^ 1]) + good[crc_at + 1:]
+    assert np.array_equal(sfrt.decode_png(flipped)[0], sfrt.decode_png(good)[0])
