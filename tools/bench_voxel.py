@@ -23,6 +23,7 @@ import voxel_scenes as vs  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -52,16 +53,17 @@ def main():
         wall = time.perf_counter() - t0
         w.check(stream.cuda_stream)
         kms = sorted(a.elapsed_time(b) for a, b in ev)[len(ev) // 2]
-        o = oracle.VoxelOracle(scene, width, height, tex, dyn, vs.COLORS)
-        t0 = time.perf_counter()
-        cpu = o.render(threads)
-        cpu_s = time.perf_counter() - t0
-        same = bool(np.array_equal(cpu, buf.cpu().numpy().ravel()))
-        res[f"{width}x{height}@{pose[0]}/{pose[1]},{pose[2]}"] = {
-            "gpu_kernel_ms_median": round(kms, 4),
-            "gpu_Mrays_per_s": round(width * height * args.steps / wall / 1e6, 1),
-            "cpu_Mrays_per_s": round(width * height / cpu_s / 1e6, 2), "cpu_threads": threads,
-            "bit_identical": same}
+        ent = {"gpu_kernel_ms_median": round(kms, 4),
+               "gpu_Mrays_per_s": round(width * height * args.steps / wall / 1e6, 1)}
+        if not args.no_cpu:
+            o = oracle.VoxelOracle(scene, width, height, tex, dyn, vs.COLORS)
+            t0 = time.perf_counter()
+            cpu = o.render(threads)
+            cpu_s = time.perf_counter() - t0
+            ent.update({"cpu_Mrays_per_s": round(width * height / cpu_s / 1e6, 2),
+                        "cpu_threads": threads,
+                        "bit_identical": bool(np.array_equal(cpu, buf.cpu().numpy().ravel()))})
+        res[f"{width}x{height}@{pose[0]}/{pose[1]},{pose[2]}"] = ent
     print(json.dumps(res, indent=1))
 
 
