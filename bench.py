@@ -5,7 +5,8 @@
 
 A step is one full frame: every rank fills its row band of a 3840 x (2160*N)
 RGBA8 frame in HBM through libsfrt.so (64-sphere cave, BASELINE config 3),
-then for N > 1 the bands are gathered to rank 0 over RCCL.  Per-GPU work is
+then for N > 1 the bands are gathered to rank 0 over RCCL, the gather of
+frame k overlapping the render of frame k+1 (double-buffered bands/frames).  Per-GPU work is
 fixed as N grows ("weak" scaling); rays use the global row index, so the
 gathered frame is byte-identical to a single-GPU render of the same frame.
 value = all rays of the K frames / (max over ranks of the timed wall time).
@@ -59,46 +60,80 @@ def band_of(rank: int, world: int, height: int) -> tuple[int, int]:
     return r0, (rank + 1) * height // world - r0
 
 
-def band_buffers(rank: int, world_size: int, height: int, pitch: int, device):
-    """Row-band buffers for one frame of `height` rows.  Rank 0 owns the whole
-    frame and renders its band in place; the gather lands every other band in
-    its slice of the frame (views, no extra copy).  Returns (band buffer,
-    frame or None, gather list or None)."""
-    row0, rows = band_of(rank, world_size, height)
-    if world_size == 1:
-        frame = torch.empty(height, pitch, dtype=torch.uint8, device=device)
-        return frame, frame, None
-    if rank == 0:
-        frame = torch.empty(height, pitch, dtype=torch.uint8, device=device)
-        views = []
-        for r in range(world_size):
-            r0, n = band_of(r, world_size, height)
-            views.append(frame[r0:r0 + n])
-        return frame[row0:row0 + rows], frame, views
-    return torch.empty(rows, pitch, dtype=torch.uint8, device=device), None, None
+class BandPipeline:
+    """Row-band frames with the gather to rank 0 overlapped with rendering.
+
+    Every rank owns `depth` band buffers; rank 0 also owns `depth` whole
+    frames.  Frame k renders into band k % depth and its gather into frame
+    k % depth is queued asynchronously (RCCL runs it on its own stream after
+    the render that produced the band), so frame k+1 renders while frame k
+    crosses xGMI.  Reusing a buffer first waits (stream-side on RCCL) for the
+    gather that last read it.  Equal bands use one gather collective; unequal
+    bands one batch of point-to-point transfers into the frame's row slices.
+    With one rank the band IS the frame and nothing is exchanged."""
+
+    def __init__(self, rank: int, world_size: int, height: int, pitch: int, device, depth: int = 2):
+        self.rank, self.world_size, self.height = rank, world_size, height
+        self.depth = depth if world_size > 1 else 1
+        self.row0, self.rows = band_of(rank, world_size, height)
+        self.frames, self.views = [], []
+        if world_size == 1:
+            self.frames = [torch.empty(height, pitch, dtype=torch.uint8, device=device)]
+            self.bands = self.frames
+        else:
+            self.bands = [torch.empty(self.rows, pitch, dtype=torch.uint8, device=device)
+                          for _ in range(self.depth)]
+            if rank == 0:
+                for _ in range(self.depth):
+                    fr = torch.empty(height, pitch, dtype=torch.uint8, device=device)
+                    self.frames.append(fr)
+                    self.views.append([fr[r0:r0 + n] for r0, n in
+                                       (band_of(r, world_size, height) for r in range(world_size))])
+        self.pending = [[] for _ in range(self.depth)]
+
+    def acquire(self, k: int):
+        """The band buffer for frame k, once the gather that last read it is done."""
+        b = k % self.depth
+        for work in self.pending[b]:
+            work.wait()
+        self.pending[b] = []
+        return self.bands[b]
+
+    def submit(self, k: int) -> None:
+        """Queue frame k's gather (after everything already queued on the current stream)."""
+        if self.world_size == 1:
+            return
+        b = k % self.depth
+        band = self.bands[b]
+        views = self.views[b] if self.rank == 0 else None
+        if self.height % self.world_size == 0:
+            self.pending[b] = [dist.gather(band, views, dst=0, async_op=True)]
+        elif self.rank == 0:
+            ops = [dist.P2POp(dist.irecv, views[r], r) for r in range(1, self.world_size)]
+            views[0].copy_(band)
+            self.pending[b] = dist.batch_isend_irecv(ops)
+        else:
+            self.pending[b] = dist.batch_isend_irecv([dist.P2POp(dist.isend, band, 0)])
+
+    def drain(self) -> None:
+        for b in range(self.depth):
+            for work in self.pending[b]:
+                work.wait()
+            self.pending[b] = []
+
+    def frame(self, k: int):
+        """Rank 0's assembled frame k (valid after drain() or the next acquire of its slot)."""
+        return self.frames[k % self.depth] if self.frames else None
 
 
-def gather_bands(buf, gather_list, rank: int, world_size: int, height: int) -> None:
-    """Bands -> rank 0.  Equal bands (height % world_size == 0): one gather
-    collective (RCCL over xGMI on the GPU node); otherwise one batch of
-    point-to-point transfers straight into the frame's row slices."""
-    if height % world_size == 0:
-        dist.gather(buf, gather_list, dst=0)
-        return
-    if rank == 0:
-        ops = [dist.P2POp(dist.irecv, gather_list[r], r) for r in range(1, world_size)]
-    else:
-        ops = [dist.P2POp(dist.isend, buf, 0)]
-    for req in dist.batch_isend_irecv(ops):
-        req.wait()
-
-
-def time_frames(world, buf, pitch, row0, rows, steps, warmup, stream, gather=None):
-    """Warmup, then `steps` timed frames.  Returns (wall seconds, kernel ms per frame)."""
-    for _ in range(warmup):
-        world.render_band(buf.data_ptr(), pitch, row0, rows, stream.cuda_stream)
-        if gather:
-            gather()
+def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream):
+    """Warmup, then `steps` timed frames through the pipeline.  Returns (wall seconds,
+    kernel ms per frame from HIP events around each render on the launch stream)."""
+    for k in range(warmup):
+        world.render_band(pipe.acquire(k).data_ptr(), pitch, pipe.row0, pipe.rows,
+                          stream.cuda_stream)
+        pipe.submit(k)
+    pipe.drain()
     world.check(stream.cuda_stream)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
@@ -107,11 +142,12 @@ def time_frames(world, buf, pitch, row0, rows, steps, warmup, stream, gather=Non
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
+        band = pipe.acquire(k)
         starts[k].record(stream)
-        world.render_band(buf.data_ptr(), pitch, row0, rows, stream.cuda_stream)
+        world.render_band(band.data_ptr(), pitch, pipe.row0, pipe.rows, stream.cuda_stream)
         ends[k].record(stream)
-        if gather:
-            gather()
+        pipe.submit(k)
+    pipe.drain()
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
@@ -170,12 +206,8 @@ def main() -> None:
     w.load_texture(*floor)
     w.set_scene(scene, WIDTH, height)
 
-    buf, frame, gather_list = band_buffers(rank, world_size, height, pitch, "cuda")
-    gather = ((lambda: gather_bands(buf, gather_list, rank, world_size, height))
-              if world_size > 1 else None)
-
-    wall, kernel_ms = time_frames(w, buf, pitch, row0, rows, args.steps, args.warmup, stream,
-                                  gather)
+    pipe = BandPipeline(rank, world_size, height, pitch, "cuda")
+    wall, kernel_ms = time_frames(w, pipe, pitch, args.steps, args.warmup, stream)
     if world_size > 1:
         t = torch.tensor([wall], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -203,7 +235,7 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic: pinned 64-sphere cave (SURVEY 8d config 3), Floor.png texels",
             "config": {"workload": f"{WIDTH}x{height} lcg64 pose(0,0), {world_size} row band(s)"
-                                   + (" + RCCL gather to rank 0" if world_size > 1 else ""),
+                                   + (" + RCCL gather to rank 0 (overlapped)" if world_size > 1 else ""),
                        "width": WIDTH, "height": height, "spheres": int(scene.spheres.shape[0]),
                        "parallelism": f"row-bands x{world_size}"},
             "kernel_ms": round(kernel_ms, 4),
@@ -227,7 +259,8 @@ def main() -> None:
                     "valu_insts_per_ray": round(meas["SQ_INSTS_VALU"] * 64 / rays_per_launch, 1),
                     "source": src}
     if world_size > 1 and rank == 0:
-        # The gathered frame must equal a single-GPU render of the whole frame.
+        # The last gathered frame must equal a single-GPU render of the whole frame.
+        frame = pipe.frame(args.steps - 1)
         single = torch.empty_like(frame)
         w.render_band(single.data_ptr(), pitch, 0, height, stream.cuda_stream)
         w.check(stream.cuda_stream)
@@ -238,15 +271,15 @@ def main() -> None:
         w2 = sfrt.World(local_rank)
         w2.load_texture(*floor)
         w2.set_scene(scenes.default10(), 1920, 1080)
-        buf2 = torch.empty(1080, 1920 * 4, dtype=torch.uint8, device="cuda")
-        wall2, k2 = time_frames(w2, buf2, 1920 * 4, 0, 1080, args.steps, args.warmup, stream)
+        pipe2 = BandPipeline(0, 1, 1080, 1920 * 4, "cuda")
+        wall2, k2 = time_frames(w2, pipe2, 1920 * 4, args.steps, args.warmup, stream)
         result["also"] = {"1920x1080_default10": {
             "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
             "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4)}}
         w2.close()
         if not args.no_cpu_baseline:
             torch.cuda.synchronize()
-            gpu_frame = buf.cpu().numpy().ravel()
+            gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()
             result["cpu_baseline"] = cpu_baseline(scene, WIDTH, height, floor, gpu_frame)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -2,8 +2,10 @@
 
 Each rank renders its row band of the frame with the CPU restatement (this is
 test infrastructure standing in for the device fill), then bench.py's own
-band_buffers / dist.gather assemble the frame on rank 0, which must equal the
-single-rank frame byte for byte.  world_size 2 and 3 (uneven band sizes).
+BandPipeline (double-buffered bands, asynchronous gather / point-to-point
+transfers to rank 0) assembles the frames on rank 0, which must equal the
+single-rank frames byte for byte -- three frames with different camera poses
+in flight without draining in between.  world_size 2 and 3 (uneven bands).
 """
 import os
 import socket
@@ -33,15 +35,20 @@ def _worker(rank, world_size, port, width, height, out_path):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world_size)
     tex, tw, th = scenes.load_floor()
-    o = oracle.Oracle.from_scene(scenes.lcg64().posed(0.4, 0.05), width, height, tex, tw, th)
     pitch = width * 4
-    buf, frame, gather_list = bench.band_buffers(rank, world_size, height, pitch, "cpu")
-    row0, rows = bench.band_of(rank, world_size, height)
-    buf.copy_(torch.from_numpy(o.render_band(row0, rows).reshape(rows, pitch)))
-    bench.gather_bands(buf, gather_list, rank, world_size, height)
+    poses = [(0.4, 0.05), (1.3, -0.2), (2.9, 0.3)]
+    oracles = [oracle.Oracle.from_scene(scenes.lcg64().posed(*p), width, height, tex, tw, th)
+               for p in poses]
+    pipe = bench.BandPipeline(rank, world_size, height, pitch, "cpu")
+    for k, o in enumerate(oracles):
+        band = pipe.acquire(k)
+        band.copy_(torch.from_numpy(o.render_band(pipe.row0, pipe.rows).reshape(pipe.rows, pitch)))
+        pipe.submit(k)
+    pipe.drain()
     if rank == 0:
-        full = o.render(2).reshape(height, pitch)
-        np.save(out_path, np.array([np.array_equal(frame.numpy(), full)]))
+        ok = [np.array_equal(pipe.frame(k).numpy(), oracles[k].render(2).reshape(height, pitch))
+              for k in (1, 2)]
+        np.save(out_path, np.array([all(ok)]))
     dist.barrier()
     dist.destroy_process_group()
 
