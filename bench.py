@@ -11,8 +11,11 @@ fixed as N grows ("weak" scaling); rays use the global row index, so the
 gathered frame is byte-identical to a single-GPU render of the same frame.
 value = all rays of the K frames / (max over ranks of the timed wall time).
 
-Also reported (rank 0, N = 1): the 1920x1080 10-sphere frame (BASELINE
-config 2), the kernel's HBM roofline from HIP events on the launch stream,
+Also reported under "also": the 7680x4320 frame row-tiled over the N ranks
+(BASELINE config 4; N = 1, 2, 4, 8) and the 16384x16384 frame on 8 ranks
+(config 5), both strong scaling with the overlapped gather; at N = 1 the
+1920x1080 10-sphere frame (config 2).  And the kernel's HBM roofline from HIP
+events on the launch stream,
 and the CPU baseline: the oracle (CPU restatement, oracle/) rendering one
 whole 4K frame on the host cores, compared byte for byte with the GPU frame.
 """
@@ -49,7 +52,10 @@ def measured_traffic(grid_threads: int):
     rocprofv3 --pmc passes of this same command), or None."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
-        ent = json.load(open(path))["per_grid_threads"].get(str(grid_threads))
+        doc = json.load(open(path))
+        if doc.get("kernel", "k_trace") != "k_trace":
+            continue
+        ent = doc["per_grid_threads"].get(str(grid_threads))
         if ent:
             return ent, os.path.relpath(path, ROOT)
     return None, None
@@ -157,6 +163,31 @@ def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream):
     return wall, kernel_ms
 
 
+def max_over_ranks(x: float) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, stream):
+    """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped gather)."""
+    world.set_scene(scene, width, height)
+    pipe = BandPipeline(rank, world_size, height, width * 4, "cuda")
+    wall, kms = time_frames(world, pipe, width * 4, steps, warmup, stream)
+    wall = max_over_ranks(wall)
+    del pipe
+    return {"n_gpus": world_size, "Mrays_per_s": round(width * height * steps / wall / 1e6, 2),
+            "fps": round(steps / wall, 2), "ms_per_frame": round(wall / steps * 1e3, 4),
+            "kernel_ms_rank0_band": round(kms, 4)}
+
+
+# BASELINE.json configs 4 and 5 (and the 8K frame on one GPU): frame size by GPU count.
+EXTRA_FRAMES = {1: [(7680, 4320)], 2: [(7680, 4320)], 4: [(7680, 4320)],
+                8: [(7680, 4320), (16384, 16384)]}
+
+
 def cpu_baseline(scene, width, height, floor, gpu_frame):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU restatement, timed as the baseline
@@ -180,6 +211,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the 8K / 16K frames")
     args = ap.parse_args()
 
     if not torch.cuda.is_available():
@@ -208,10 +240,7 @@ def main() -> None:
 
     pipe = BandPipeline(rank, world_size, height, pitch, "cuda")
     wall, kernel_ms = time_frames(w, pipe, pitch, args.steps, args.warmup, stream)
-    if world_size > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = max_over_ranks(wall)
     total_rays = WIDTH * height * args.steps
     value = total_rays / wall / 1e6
     ms_per_step = wall / args.steps * 1e3
@@ -266,6 +295,16 @@ def main() -> None:
         w.check(stream.cuda_stream)
         result["gathered_frame_bit_identical"] = bool(torch.equal(single, frame))
         del single
+    # Larger frames of the BASELINE configs (strong scaling: the frame is fixed,
+    # its rows split over the ranks), measured after the main line.
+    extra = {}
+    if not args.no_extra:
+        for fw, fh in EXTRA_FRAMES.get(world_size, []):
+            extra[f"{fw}x{fh}_lcg64"] = measure_frame(w, scene, fw, fh, rank, world_size,
+                                                      max(5, args.steps // 2), 2, stream)
+        w.set_scene(scene, WIDTH, height)
+    if rank == 0:
+        result["also"] = dict(extra)
     if world_size == 1:
         # BASELINE config 2: 1920x1080, 10-sphere scene.
         w2 = sfrt.World(local_rank)
@@ -273,9 +312,9 @@ def main() -> None:
         w2.set_scene(scenes.default10(), 1920, 1080)
         pipe2 = BandPipeline(0, 1, 1080, 1920 * 4, "cuda")
         wall2, k2 = time_frames(w2, pipe2, 1920 * 4, args.steps, args.warmup, stream)
-        result["also"] = {"1920x1080_default10": {
-            "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
-            "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4)}}
+        result["also"]["1920x1080_default10"] = {
+            "n_gpus": 1, "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
+            "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4)}
         w2.close()
         if not args.no_cpu_baseline:
             torch.cuda.synchronize()

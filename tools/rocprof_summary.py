@@ -1,6 +1,7 @@
 """Summarise rocprofv3 CSV output of bench.py runs into profiles/.
 
-    python tools/rocprof_summary.py --trace DIR --fetch DIR --write DIR --tag r1 [--out profiles]
+    python tools/rocprof_summary.py --trace DIR --fetch DIR --write DIR --tag r1 [--sq DIR]
+                                    [--kernel k_trace|k_glsl|k_voxel] [--out profiles]
 
 Writes
   profiles/<tag>_kernel_stats_by_grid.csv  per (kernel, grid size): calls, avg/min/max ns
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--sq", help="--pmc pass with SQ_INSTS_VALU / SQ_WAVES")
     ap.add_argument("--tag", required=True)
+    ap.add_argument("--kernel", default="k_trace", help="kernel-name substring (k_trace, k_glsl, k_voxel)")
     ap.add_argument("--out", default="profiles")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -51,14 +53,14 @@ def main():
     for d, counter in ((a.fetch, "FETCH_SIZE"), (a.write, "WRITE_SIZE")):
         acc = collections.defaultdict(list)
         for r in rows(d, "counter_collection"):
-            if "k_trace" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if a.kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 acc[int(r["Grid_Size"])].append(float(r["Counter_Value"]) * 1024.0)
         for grid, v in acc.items():
             traffic.setdefault(str(grid), {})[counter] = sum(v) / len(v)
     if a.sq:
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in rows(a.sq, "counter_collection"):
-            if "k_trace" in r["Kernel_Name"]:
+            if a.kernel in r["Kernel_Name"]:
                 acc[int(r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for grid, cs in acc.items():
             for c, v in cs.items():
@@ -67,8 +69,8 @@ def main():
         t["hbm_bytes_per_launch"] = 2.0 * t.get("FETCH_SIZE", 0.0) + t.get("WRITE_SIZE", 0.0)
         t["algorithmic_bytes_per_launch"] = 4.0 * int(g)
     with open(os.path.join(a.out, f"{a.tag}_traffic.json"), "w") as f:
-        json.dump({"note": __doc__.split("Writes")[0].strip(), "per_grid_threads": traffic}, f,
-                  indent=1)
+        json.dump({"note": __doc__.split("Writes")[0].strip(), "kernel": a.kernel,
+                   "per_grid_threads": traffic}, f, indent=1)
     print(json.dumps(traffic, indent=1))
 
 
