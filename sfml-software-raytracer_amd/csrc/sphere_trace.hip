@@ -162,13 +162,21 @@ __device__ __forceinline__ void pass_body(bool pass, float ss, float r, int k, f
   // Scalar branch around the sqrt: most culled spheres pass for no lane of
   // the wave in a given step, and then the whole body is skipped (the
   // compiler would otherwise if-convert it and run the sqrt every time).
-  if (__builtin_amdgcn_ballot_w64(pass)) {
+  const uint64_t pm = __builtin_amdgcn_ballot_w64(pass);
+  if (pm) {
     __asm__ volatile("; sphere passes for some lane");  // keeps the branch (no if-conversion)
-    const bool tiny = __builtin_amdgcn_ballot_w64(pass && ss < kTinySqrtArg) != 0;
-    if (pass) {
-      const float d = tiny ? __builtin_sqrtf(ss) : sqrt_cr_normal(ss);
-      const float t = r - d;
-      L = L < t ? t : L;  // std::max(largestDist, t)
+    // Uniform choice of the sqrt sequence: ballots of plain compares combined
+    // in SALU (a ballot of `pass && tiny`, or a bool select, is rematerialised
+    // through VGPRs on every visit).
+    if ((__builtin_amdgcn_ballot_w64(ss < kTinySqrtArg) & pm) == 0) {
+      if (pass) {
+        const float t = r - sqrt_cr_normal(ss);
+        L = L < t ? t : L;  // std::max(largestDist, t)
+        dnew = k;
+      }
+    } else if (pass) {
+      const float t = r - __builtin_sqrtf(ss);
+      L = L < t ? t : L;
       dnew = k;
     }
   }
@@ -191,7 +199,8 @@ __device__ __forceinline__ void sphere_step(float px, float py, float pz, float 
 }
 
 template <bool INLINE, int SLOTS>
-__device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* __restrict__ sph) {
+__device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* __restrict__ sph,
+                                           const SphereRec* __restrict__ rest_sph) {
   __shared__ uint64_t s_mask[kWavesPerBlock][kMaskWords];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -218,11 +227,14 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
   float py = f.cam[1] + dy * l0;
   float pz = f.cam[2] + dz * l0;
   int draw = f.first_draw;
-  bool active = valid && l0 > 0.0f;
+  // March state as a float: the lane's last step length (> 0 while it marches;
+  // 0 once it stopped or for lanes that never march).  `mv > 0` is one compare
+  // per step, where a loop-carried bool is rematerialised through VGPRs.
+  float mv = (valid && l0 > 0.0f) ? 1.0f : 0.0f;
 
   // ---- per-wave sphere cull (the "wavefront ballot") ----
   const int nwords = (f.n + 63) >> 6;
-  const bool any_march = __builtin_amdgcn_ballot_w64(active) != 0;
+  const bool any_march = __builtin_amdgcn_ballot_w64(mv > 0.0f) != 0;
   Cone cone{};
   if (f.cull && any_march) cone = tile_cone(f, tile_x, tile_y, dx, dy, dz);
   auto word_mask = [&](int w) -> uint64_t {
@@ -250,7 +262,7 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
     }
     uint64_t rest = m;  // culled spheres beyond the slots (higher indices)
     int trips = 1;
-    while (__builtin_amdgcn_ballot_w64(active)) {
+    while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
       if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
 #pragma unroll
         for (int q = 0; q < SLOTS; q++) ssp[q] = 0.0f;  // slots never pass again
@@ -268,18 +280,18 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
       for (int q = 0; q < SLOTS; q++) pass_body(ssq[q] < ssp[q], ssq[q], sr[q], sk[q], L, dnew);
       for (uint64_t mm = rest; mm; mm &= mm - 1) {
         const int k = __builtin_ctzll(mm);
-        const SphereRec& s = sph[k];
+        const SphereRec& s = rest_sph[k];
         sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
       }
-      if (active) {
+      if (mv > 0.0f) {
         px = px + dx * L;
         py = py + dy * L;
         pz = pz + dz * L;
         draw = dnew;
-        active = L > 0.0f;
+        mv = L;  // L >= 0: max(0, r - d) over passing spheres
       }
       if (++trips >= kMaxIterations) {
-        if (active) atomicOr(f.status, 1);
+        if (mv > 0.0f) atomicOr(f.status, 1);
         break;
       }
     }
@@ -293,7 +305,7 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
     __builtin_amdgcn_wave_barrier();
     int trips = 1;
     bool full = !(f.cull && any_march);
-    while (__builtin_amdgcn_ballot_w64(active)) {
+    while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
       if (trips == kCullSafeIterations) full = true;
       float L = 0.0f;
       int dnew = draw;
@@ -313,15 +325,15 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
           sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
         }
       }
-      if (active) {
+      if (mv > 0.0f) {
         px = px + dx * L;
         py = py + dy * L;
         pz = pz + dz * L;
         draw = dnew;
-        active = L > 0.0f;
+        mv = L;  // L >= 0: max(0, r - d) over passing spheres
       }
       if (++trips >= kMaxIterations) {
-        if (active) atomicOr(f.status, 1);
+        if (mv > 0.0f) atomicOr(f.status, 1);
         break;
       }
     }
@@ -332,13 +344,20 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
   f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
 }
 
-template <int SLOTS>
+template <int SLOTS, bool REST_LDS>
 __global__ __launch_bounds__(256) void k_trace_inline(InlineArgs args) {
-  trace_tile<true, SLOTS>(args.f, args.s);
+  if (REST_LDS) {  // spheres beyond the slots read from an LDS copy instead of s_load
+    __shared__ SphereRec lsph[kInlineSpheres];
+    for (int t = threadIdx.x; t < args.f.n; t += blockDim.x) lsph[t] = args.s[t];
+    __syncthreads();
+    trace_tile<true, SLOTS>(args.f, args.s, lsph);
+  } else {
+    trace_tile<true, SLOTS>(args.f, args.s, args.s);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_trace_global(FrameRec f) {
-  trace_tile<false, 0>(f, f.spheres);
+  trace_tile<false, 0>(f, f.spheres, f.spheres);
 }
 
 // Debug/parity kernel: one lane per listed pixel, full sphere list, float
@@ -396,10 +415,12 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     // SFRT_OPT_VARIANT (tuning A/B only): number of SGPR sphere slots; 0 = kSlots.
     const dim3 g((unsigned)blocks), b(256);
     switch (f.variant) {
-      case 1: hipLaunchKernelGGL(k_trace_inline<0>, g, b, 0, s, args); break;
-      case 6: hipLaunchKernelGGL(k_trace_inline<6>, g, b, 0, s, args); break;
-      case 8: hipLaunchKernelGGL(k_trace_inline<8>, g, b, 0, s, args); break;
-      default: hipLaunchKernelGGL(k_trace_inline<kSlots>, g, b, 0, s, args); break;
+      case 1: hipLaunchKernelGGL((k_trace_inline<0, false>), g, b, 0, s, args); break;
+      case 6: hipLaunchKernelGGL((k_trace_inline<6, false>), g, b, 0, s, args); break;
+      case 8: hipLaunchKernelGGL((k_trace_inline<8, false>), g, b, 0, s, args); break;
+      case 16: hipLaunchKernelGGL((k_trace_inline<kSlots, true>), g, b, 0, s, args); break;
+      case 17: hipLaunchKernelGGL((k_trace_inline<0, true>), g, b, 0, s, args); break;
+      default: hipLaunchKernelGGL((k_trace_inline<kSlots, false>), g, b, 0, s, args); break;
     }
   } else {
     hipLaunchKernelGGL(k_trace_global, dim3((unsigned)blocks), dim3(256), 0, s, f);

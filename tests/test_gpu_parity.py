@@ -95,6 +95,21 @@ def test_cull_on_off_identical(world, floor):
     assert diff_report(a, b, 3840) == ""
 
 
+@pytest.mark.parametrize("variant", [1, 6, 8, 16, 17])
+def test_kernel_variants_identical(world, floor, variant):
+    """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
+    produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
+    import sfrt
+    world.set_scene(scenes.lcg64().posed(1.1, -0.2), 3840, 2160)
+    a = world.render()
+    world.set_option(sfrt.SFRT_OPT_VARIANT, variant)
+    try:
+        b = world.render()
+    finally:
+        world.set_option(sfrt.SFRT_OPT_VARIANT, 0)
+    assert diff_report(a, b, 3840) == ""
+
+
 @pytest.mark.parametrize("ystart,yadd,xstart,xadd", [
     (0, 8, 0, 4), (3, 8, 2, 4), (7, 8, 3, 4),   # RenderThread interleave (Source.cpp:21,23)
     (1, 3, 0, 1), (0, 1, 5, 7), (239, 1, 319, 1), (5, 1000, 0, 1)])
