@@ -250,6 +250,8 @@ SFRT_API int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int heigh
 /* rt.draw + rt.getTexture().copyToImage() into a host RGBA8 buffer (synchronous). */
 SFRT_API int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height);
 SFRT_API int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream);
+/* SFRT_OPT_VARIANT: kernel variant for A/B timing (same bytes; tests check it). */
+SFRT_API int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value);
 
 /* ======================================================================
  * Asset pipeline: PNG -> RGBA8 as sf::Image::loadFromFile

@@ -50,7 +50,9 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
   return (uint32_t)(int)floorf(v * 255.0f + 0.5f);
 }
 
-__device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
+template <bool LDS>
+__device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __restrict__ walls,
+                                         const GlslBall* __restrict__ balls, int i, int row) {
   const float fx = (float)i + 0.5f;
   const float fy = (float)(f.height - 1 - row) + 0.5f;
   const float ax = -f.fov_x + f.hk * fx;                                   // :172-173
@@ -70,12 +72,18 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
   float px = cx, py = cy, pz = cz;
   int draw = 0;
   float total = 0.0f;
-  for (int j = 0, k = 0; j < 3 * f.sc; j++) {
-    const GlslWall w = f.walls[k];
+  // Iterations before wall_start leave every lane at campos outside the wall
+  // (host-checked with the same test), so they change nothing; a whole pass
+  // in which no lane of the wave is inside a wall leaves the state at a fixed
+  // point, so the remaining passes would repeat it and are skipped.
+  bool moved = false;
+  for (int j = f.wall_start, k = f.wall_start % (f.sc > 0 ? f.sc : 1); j < 3 * f.sc; j++) {
+    const GlslWall w = walls[k];
     const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
     const float s = (rx * rx + ry * ry) + rz * rz;
     const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
     if (__builtin_amdgcn_ballot_w64(inside)) {
+      moved = true;
       const float cs = inside ? 1.0f : 0.0f;
       const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
       const float c = cs * s - w.rr;
@@ -94,7 +102,11 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
       pz = pz + dz * 0.0f;
     }
     draw = inside ? k : draw;
-    if (++k == f.sc) k = 0;
+    if (++k == f.sc) {
+      k = 0;
+      if (!moved) break;  // uniform
+      moved = false;
+    }
   }
 
   // ---- metaball march over lights + ospheres (:87-112) ----
@@ -114,8 +126,11 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
     closest = 0;
     float shortest = 9999999.0f;
     snx = sny = snz = 0.0f;
+    // Dominance threshold t*(1+1e-5) + 1e-4, t = max(smooth + 0.5, shortest,
+    // 0.5); it only changes when a ball's body runs.
+    float thr = 1e30f;
     for (int k = 0; k < nballs; k++) {
-      const GlslBall b = f.balls[k];
+      const GlslBall b = balls[k];
       const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
       const float ss = (ox * ox + oy * oy) + oz * oz;
       // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
@@ -123,8 +138,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
       // normalFactor == 1, so the body changes nothing (smoothNormal at most
       // flips the sign of a zero component, which no output depends on).
       // Tested on the squared length with relative margins.
-      const float t = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f);
-      const float bnd = (b.r_skip + t * 1.00001f) + 1e-4f;
+      const float bnd = b.r_skip + thr;
       const bool dominated = ss >= bnd * bnd * 1.00001f;
       if (!__builtin_amdgcn_ballot_w64(!dominated)) continue;
       const float other = sqrt_cr(ss) - b.r;
@@ -136,6 +150,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
       snx = nf * snx - (1.0f - nf) * ox;
       sny = nf * sny - (1.0f - nf) * oy;
       snz = nf * snz - (1.0f - nf) * oz;
+      thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * 1.00001f + 1e-4f;
     }
     ball_dist += smooth + 0.01f;
   }
@@ -183,7 +198,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
                        ((float)(f.sc + f.lc - 1) < (float)draw ? 0.0f : 1.0f);
   const int nshadow = f.all - f.sc - f.lc;
   for (int li = 0; li < f.lc; li++) {
-    const GlslBall L = f.balls[li];
+    const GlslBall L = balls[li];
     const float tlx = L.x - px, tly = L.y - py, tlz = L.z - pz;
     const float tll = len3(tlx, tly, tlz);
     const float tnx = tlx / tll, tny = tly / tll, tnz = tlz / tll;
@@ -226,14 +241,26 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, int i, int row) {
       unorm8(cr) | (unorm8(cg) << 8) | (unorm8(cbl) << 16) | (255u << 24);
 }
 
+// Wall and ball records are read once per visit by every wave, with scalar
+// loads (wave-uniform addresses, scalar cache).  Variant 1 stages them in LDS
+// instead (one copy per workgroup); measured slower on MI355X
+// (profiles/r1_glsl_variants.json), kept for A/B.
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
+  __shared__ GlslWall s_walls[LDS ? kGlslMax : 1];
+  __shared__ GlslBall s_balls[LDS ? kGlslMax : 1];
+  if (LDS) {
+    for (int t = threadIdx.x; t < f.sc; t += blockDim.x) s_walls[t] = f.walls[t];
+    for (int t = threadIdx.x; t < f.all - f.sc; t += blockDim.x) s_balls[t] = f.balls[t];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int tx = tile % f.tiles_x, ty = tile / f.tiles_x;
   const int i = tx * 8 + (lane & 7);
   const int r = ty * 8 + (lane >> 3);
   if (i >= f.width || r >= f.rows) return;
-  fragment(f, i, f.row0 + r);
+  fragment<LDS>(f, LDS ? s_walls : f.walls, LDS ? s_balls : f.balls, i, f.row0 + r);
 }
 
 }  // namespace
@@ -243,7 +270,10 @@ int launch_glsl(const GlslFrame& f, void* stream) {
   const long long tiles = (long long)f.tiles_x * tiles_y;
   if (tiles == 0) return 0;
   const dim3 g((unsigned)((tiles + 3) / 4)), b(256);
-  hipLaunchKernelGGL(k_glsl, g, b, 0, (hipStream_t)stream, f);
+  if (f.variant == 1)
+    hipLaunchKernelGGL(k_glsl<true>, g, b, 0, (hipStream_t)stream, f);
+  else
+    hipLaunchKernelGGL(k_glsl<false>, g, b, 0, (hipStream_t)stream, f);
   return hipGetLastError() != hipSuccess;
 }
 

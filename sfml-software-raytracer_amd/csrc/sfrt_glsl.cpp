@@ -107,6 +107,7 @@ struct sfrt_glsl {
   int device = 0;
   sfrt_glsl_uniforms u{};
   int ground_w = 0, ground_h = 0;
+  int variant = 0;                     // SFRT_OPT_VARIANT (tuning A/B)
   // device resources
   hipStream_t stream = nullptr;
   uint32_t* d_mip = nullptr;
@@ -200,6 +201,7 @@ struct sfrt_glsl {
     f.sc = sc;
     f.lc = lc;
     f.all = all;
+    f.variant = variant;
     f.cam_negzero = (std::signbit(v.campos[0]) && v.campos[0] == 0.0f) ||
                     (std::signbit(v.campos[1]) && v.campos[1] == 0.0f) ||
                     (std::signbit(v.campos[2]) && v.campos[2] == 0.0f);
@@ -209,6 +211,19 @@ struct sfrt_glsl {
     for (int k = 0; k < sc; k++) {
       const float* S = v.spheres[k];
       walls[k] = {S[0], S[1], S[2], S[3], S[3] * S[3], inside_bound(S[3]), 0.0f, 0.0f};
+    }
+    // Every lane starts at campos: the wall-pass iterations before the first
+    // wall containing campos (same test as the kernel) are no-ops for all of
+    // them.  With a -0.0 in campos the kernel's literal update runs from 0.
+    f.wall_start = 0;
+    if (!f.cam_negzero && sc > 0) {
+      int j = 0;
+      for (; j < sc; j++) {
+        const float rx = v.campos[0] - walls[j].x, ry = v.campos[1] - walls[j].y,
+                    rz = v.campos[2] - walls[j].z;
+        if ((rx * rx + ry * ry) + rz * rz <= walls[j].s_in) break;
+      }
+      f.wall_start = j < sc ? j : 3 * sc;  // inside no wall: no lane ever moves
     }
     std::vector<sfrt::GlslBall> balls(nb > 0 ? nb : 1);
     for (int k = 0; k < nb; k++) {
@@ -472,6 +487,16 @@ int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
   if ((rc = g->launched(g->stream))) return rc;
   HIP_TRY(hipMemcpyAsync(pixels, g->d_frame, px * 4, hipMemcpyDeviceToHost, g->stream));
   return g->read_status(g->stream);
+}
+
+int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value) {
+  if (!g) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (option == SFRT_OPT_VARIANT) {
+    g->variant = value;
+    return SFRT_OK;
+  }
+  return SFRT_E_INVALID;
 }
 
 int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream) {

@@ -42,7 +42,7 @@ ABI_SYMBOLS = (
     "sfrt_voxel_check",
     "sfrt_glsl_create", "sfrt_glsl_destroy", "sfrt_glsl_set_ground", "sfrt_glsl_set_uniforms",
     "sfrt_glsl_get_uniforms", "sfrt_glsl_set_uniform", "sfrt_glsl_set_uniform_int",
-    "sfrt_glsl_draw", "sfrt_glsl_draw_image", "sfrt_glsl_check",
+    "sfrt_glsl_draw", "sfrt_glsl_draw_image", "sfrt_glsl_check", "sfrt_glsl_set_option",
     "sfrt_png_info", "sfrt_png_decode",
 )
 
@@ -142,6 +142,7 @@ def lib() -> ctypes.CDLL:
         "sfrt_glsl_draw": ([vp, vp, c_int, c_int, ctypes.c_int64, c_int, c_int, vp], c_int),
         "sfrt_glsl_draw_image": ([vp, vp, c_int, c_int], c_int),
         "sfrt_glsl_check": ([vp, vp], c_int),
+        "sfrt_glsl_set_option": ([vp, c_int, c_int], c_int),
         "sfrt_png_info": ([vp, ctypes.c_int64, P(c_int), P(c_int)], c_int),
         "sfrt_png_decode": ([vp, ctypes.c_int64, vp, ctypes.c_int64, P(c_int), P(c_int)], c_int),
     }
@@ -495,3 +496,6 @@ class GlslShader:
 
     def check(self, stream: int = 0) -> None:
         _check(lib().sfrt_glsl_check(self._h, ctypes.c_void_p(stream or None)), "glsl_check")
+
+    def set_option(self, option: int, value: int) -> None:
+        _check(lib().sfrt_glsl_set_option(self._h, option, value), "glsl_set_option")

@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--variants", default="0", help="SFRT_OPT_VARIANT values to time")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -39,33 +40,41 @@ def main():
         u = gs.default_uniforms(width, height, *rot, frames=frames)
         s.set_uniforms(u)
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
-        for _ in range(3):
-            s.draw(buf.data_ptr(), width, height, width * 4, 0, height, stream.cuda_stream)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for a, b in ev:
-            a.record(stream)
-            s.draw(buf.data_ptr(), width, height, width * 4, 0, height, stream.cuda_stream)
-            b.record(stream)
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-        s.check(stream.cuda_stream)
-        kms = sorted(a.elapsed_time(b) for a, b in ev)[len(ev) // 2]
-        ent = {"gpu_kernel_ms_median": round(kms, 4),
-               "gpu_Mfrags_per_s": round(width * height * args.steps / wall / 1e6, 1),
-               "gpu_Mfrags_per_s_kernel": round(width * height / kms / 1e3, 1)}
-        if not args.no_cpu:
-            o = oracle.GlslOracle(u, *floor)
-            t0 = time.perf_counter()
-            cpu = o.render(width, height, threads)
-            cpu_s = time.perf_counter() - t0
-            ent.update({"cpu_Mfrags_per_s": round(width * height / cpu_s / 1e6, 2),
-                        "cpu_threads": threads,
-                        "bit_identical": bool(np.array_equal(cpu, buf.cpu().numpy().ravel()))})
-        res[f"{width}x{height}@{rot[0]:g},{rot[1]:g}/frames{frames}"] = ent
+        for var in [int(v) for v in args.variants.split(",")]:
+            s.set_option(sfrt.SFRT_OPT_VARIANT, var)
+            res.update(time_one(s, buf, width, height, u, rot, frames, var, args, stream, floor,
+                                threads, oracle))
     print(json.dumps(res, indent=1))
+
+
+def time_one(s, buf, width, height, u, rot, frames, var, args, stream, floor, threads, oracle):
+    """Kernel time (HIP events, median) and wall rate of one frame size and variant."""
+    for _ in range(3):
+        s.draw(buf.data_ptr(), width, height, width * 4, 0, height, stream.cuda_stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        s.draw(buf.data_ptr(), width, height, width * 4, 0, height, stream.cuda_stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    s.check(stream.cuda_stream)
+    kms = sorted(a.elapsed_time(b) for a, b in ev)[len(ev) // 2]
+    ent = {"gpu_kernel_ms_median": round(kms, 4),
+           "gpu_Mfrags_per_s": round(width * height * args.steps / wall / 1e6, 1),
+           "gpu_Mfrags_per_s_kernel": round(width * height / kms / 1e3, 1)}
+    if not args.no_cpu:
+        o = oracle.GlslOracle(u, *floor)
+        t0 = time.perf_counter()
+        cpu = o.render(width, height, threads)
+        cpu_s = time.perf_counter() - t0
+        ent.update({"cpu_Mfrags_per_s": round(width * height / cpu_s / 1e6, 2),
+                    "cpu_threads": threads,
+                    "bit_identical": bool(np.array_equal(cpu, buf.cpu().numpy().ravel()))})
+    return {f"{width}x{height}@{rot[0]:g},{rot[1]:g}/frames{frames}/v{var}": ent}
 
 
 if __name__ == "__main__":
