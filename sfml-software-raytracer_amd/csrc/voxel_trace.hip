@@ -8,6 +8,7 @@
 // (out-of-range and NaN give INT_MIN / 0) emulated explicitly.
 #include <hip/hip_runtime.h>
 
+#include "sfrt_math.h"
 #include "voxel_trace.h"
 
 #pragma clang fp contract(off)
@@ -56,12 +57,24 @@ __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, ui
   return t.texels[idx];
 }
 
+// The DDA divides by the same |dir| components at every step.  With their
+// correctly rounded reciprocals, sfrt_math::div_recip gives the same bits as
+// the division for b in [2^-60, 2^60]; a wave with any lane
+// outside that range (an axis-parallel ray has |dir.x| == 0) divides plainly.
+__device__ __forceinline__ bool recip_ok(float b) { return b >= 0x1.0p-60f && b <= 0x1.0p60f; }
+
+template <bool RECIP>
+__device__ __forceinline__ float dv(float a, float b, float y) {
+  return RECIP ? sfrt_math::div_recip(a, b, y) : a / b;
+}
+
 __device__ __forceinline__ uint32_t pack(uint32_t r, uint32_t g, uint32_t b, uint32_t a) {
   return r | (g << 8) | (b << 16) | (a << 24);
 }
 
 // World::LRaycast, World.cpp:455-491.
-__device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
+template <bool RECIP>
+__device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
   float dist = 0.0f;
   int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
   const float dirxadd = dir.x > 0 ? 1.0f : 0.0f, diryadd = dir.y > 0 ? 1.0f : 0.0f,
@@ -69,13 +82,15 @@ __device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
   const float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
               sz = dir.z > 0 ? -1.0f : 1.0f;
   const float lx = fabsf(dir.x), ly = fabsf(dir.y), lz = fabsf(dir.z);
+  const float yx = RECIP ? 1.0f / lx : 0.0f, yy = RECIP ? 1.0f / ly : 0.0f,
+              yz = RECIP ? 1.0f / lz : 0.0f;
   const float m2 = maxDist * 2;
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
     if (block_at(f, pix, piy, piz) != kVoxEmpty) return false;
-    const float a = (dirxadd + sx * (pos.x - (float)pix)) / lx;
-    const float b = (diryadd + sy * (pos.y - (float)piy)) / ly;
-    const float c = (dirzadd + sz * (pos.z - (float)piz)) / lz;
+    const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
+    const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
+    const float c = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
     float raySpeed = a;  // std::min({a, b, c})
     if (b < raySpeed) raySpeed = b;
     if (c < raySpeed) raySpeed = c;
@@ -89,8 +104,15 @@ __device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
   return dist >= maxDist;
 }
 
+__device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
+  const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
+  if (__builtin_amdgcn_ballot_w64(!ok)) return lraycast_t<false>(f, pos, dir, maxDist);
+  return lraycast_t<true>(f, pos, dir, maxDist);
+}
+
 // World::Raycast, World.cpp:302-453.
-__device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_dir) {
+template <bool RECIP>
+__device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale, float atan_dir) {
   const V3 cam{f.cam[0], f.cam[1], f.cam[2]};
   float dist = 0.0f;
   V3 pos = cam;
@@ -101,13 +123,15 @@ __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_
   float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
         sz = dir.z > 0 ? -1.0f : 1.0f;   // dir*sign (short, exact as float)
   const float lx = fabsf(dir.x), ly = fabsf(dir.y), lz = fabsf(dir.z);
+  const float yx = RECIP ? 1.0f / lx : 0.0f, yy = RECIP ? 1.0f / ly : 0.0f,
+              yz = RECIP ? 1.0f / lz : 0.0f;
   int DI = 0;
   float raySpeed = 0.0f;
   int colRay = 0;
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
-    const float xray = (dirxadd + sx * (pos.x - (float)pix)) / lx;
-    const float yray = (diryadd + sy * (pos.y - (float)piy)) / ly;
-    const float zray = (dirzadd + sz * (pos.z - (float)piz)) / lz;
+    const float xray = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
+    const float yray = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
+    const float zray = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
     if (xray <= yray && xray <= zray) {
       raySpeed = xray;
       tryPos.x += dir.x * (raySpeed + 0.002f);
@@ -221,6 +245,12 @@ __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_
     }
   }
   return pack(0, 0, 0, 255);  // sf::Color::Black
+}
+
+__device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_dir) {
+  const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
+  if (__builtin_amdgcn_ballot_w64(!ok)) return raycast_t<false>(f, dir, yscale, atan_dir);
+  return raycast_t<true>(f, dir, yscale, atan_dir);
 }
 
 // 16x16 pixels per 256-thread workgroup.

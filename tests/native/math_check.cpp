@@ -5,6 +5,7 @@
 //   ./math_check atan2f <npairs> <seed> -> random + structured pairs
 //   ./math_check atan2f_x1 | atan2f_y1  -> atan2f(y, 1) / atan2f(1, x) for every binary32
 //   ./math_check divpi                  -> q/PI2 + 1 and q/PI + 0.5 for every finite q
+//   ./math_check divrecip <n>           -> div_recip(a, b, 1/b) == a/b on n random pairs
 // Prints "<fn> checked=<n> mismatches=<m>" and the first mismatches.
 #include <cmath>
 #include <cstdint>
@@ -107,6 +108,36 @@ int main(int argc, char** argv) {
         if (bad < 5) {
 #pragma omp critical
           printf("MISMATCH atan2f(%a, %a) libm=%a sfrt=%a\n", y, x, want, got);
+        }
+        bad++;
+      }
+    }
+  } else if (!strcmp(fn, "divrecip")) {
+    // sfrt_math::div_recip(a, b, 1/b) == a / b over random normal pairs and the
+    // voxel DDA domain (b in (2^-14, 1.5], a in [-0.25, 1.25]).
+    const long long n = argc > 2 ? atoll(argv[2]) : 100000000LL;
+#pragma omp parallel for reduction(+ : bad, checked) schedule(static)
+    for (long long k = 0; k < n; k++) {
+      uint64_t z = (uint64_t)k * 0x9E3779B97F4A7C15ULL + 77;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+      z ^= z >> 31;
+      float a, b;
+      if (k & 1) {
+        const uint32_t eb = 127 - 60 + (uint32_t)((z >> 40) % 121);
+        const uint32_t ea = eb - 40 + (uint32_t)((z >> 48) % 81);
+        b = fl((eb << 23) | ((uint32_t)z & 0x7fffffu) | (uint32_t)((z >> 63) << 31));
+        a = fl((ea << 23) | ((uint32_t)(z >> 20) & 0x7fffffu) | (uint32_t)(((z >> 62) & 1) << 31));
+      } else {
+        b = 1.5f * ((float)((uint32_t)z >> 8) / 16777216.0f);
+        if (b < 0x1.0p-14f) b = 0x1.0p-14f;
+        a = -0.25f + 1.5f * ((float)((uint32_t)(z >> 32) >> 8) / 16777216.0f);
+      }
+      checked++;
+      if (!same(a / b, sfrt_math::div_recip(a, b, 1.0f / b))) {
+        if (bad < 5) {
+#pragma omp critical
+          printf("MISMATCH divrecip a=%a b=%a\n", a, b);
         }
         bad++;
       }

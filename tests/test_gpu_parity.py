@@ -221,6 +221,16 @@ def test_device_math_matches_libm(fn, arg, tmp_path):
     assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
 
 
+def test_device_div_recip(tmp_path):
+    """sfrt_math::div_recip(a, b, 1/b) == a / b on gfx950 (3 x 2^33 pairs, DESIGN.md 4)."""
+    exe = tmp_path / "div_check"
+    src = os.path.join(ROOT, "tests", "native", "div_check.hip")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    "-ffp-contract=off", src, "-o", str(exe)], check=True, capture_output=True)
+    r = subprocess.run([str(exe), "33"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
+
+
 def test_pipelined_frames_match_update_image(world, floor):
     """Display path: two frames in flight, camera changing per frame."""
     import sfrt

@@ -24,7 +24,8 @@ def math_check(tmp_path_factory):
 
 
 @pytest.mark.parametrize("args", [["asinf"], ["atanf"], ["acosf"], ["atan2f", "100000000", "1"],
-                                  ["atan2f_x1"], ["atan2f_y1"], ["divpi"]])
+                                  ["atan2f_x1"], ["atan2f_y1"], ["divpi"],
+                                  ["divrecip", "1000000000"]])
 def test_restated_math_matches_libm(math_check, args):
     r = subprocess.run([math_check] + args, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
