@@ -197,12 +197,22 @@ def cpu_baseline(scene, width, height, floor, gpu_frame):
     frame = o.render(threads)
     dt = time.perf_counter() - t0
     same = bool(np.array_equal(frame, gpu_frame))
+    # One thread on every 16th row (the reference's UpdateImage(img, 0, 16, 0, 1)).
+    sub = np.zeros(width * height * 4, dtype=np.uint8)
+    t1 = time.perf_counter()
+    o.update_image(sub, 0, 16, 0, 1)
+    dt1 = time.perf_counter() - t1
+    rows1 = (height + 15) // 16
+    same1 = bool(np.array_equal(sub.reshape(height, -1)[::16], gpu_frame.reshape(height, -1)[::16]))
     return {"value": round(width * height / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads,
             "kind": "port",
             "sample": f"one full {width}x{height} frame of the same scene, oracle/sphereworld_oracle.c "
                       f"(-O2, no FMA), {threads} threads with the reference's row interleave "
                       f"(Source.cpp:21), {dt:.2f} s",
-            "frame_bit_identical_to_gpu": same}
+            "frame_bit_identical_to_gpu": same,
+            "single_thread": {"value": round(width * rows1 / dt1 / 1e6, 3), "unit": "Mrays/s",
+                              "cores": 1, "sample": f"rows j % 16 == 0 ({rows1} rows), {dt1:.2f} s",
+                              "bit_identical_to_gpu": same1}}
 
 
 def main() -> None:
