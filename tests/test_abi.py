@@ -3,6 +3,7 @@ declares, and its host-side helpers agree with the restatement."""
 import ctypes
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -110,3 +111,16 @@ def test_lcg64_scene_shape():
     # first draws of the MSVC LCG, seed 12345 (s = s*214013 + 2531011, r = (s >> 16) & 0x7fff)
     st, r = scenes.msvc_rand(12345)
     assert r == ((12345 * 214013 + 2531011) & 0xFFFFFFFF) >> 16 & 0x7FFF
+
+
+def test_cpp_header_builds(built, tmp_path):
+    """include/sfrt.hpp (the C++ mirror of SphereWorld / World / sf::Shader) compiles and
+    links against libsfrt.so; run on the GPU by test_gpu_parity.py::test_cpp_host_api."""
+    lib_dir = os.path.join(ROOT, "sfml-software-raytracer_amd")
+    exe = tmp_path / "cpp_api_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I",
+                    os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "cpp_api_check.cpp"), "-L", lib_dir,
+                    "-lsfrt", f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath-link,/opt/rocm/lib",
+                    "-lpthread", "-o", str(exe)], check=True)
+    assert exe.exists()

@@ -231,6 +231,24 @@ def test_device_div_recip(tmp_path):
     assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
 
 
+def test_cpp_host_api(built, tmp_path):
+    """include/sfrt.hpp driven from C++ like the reference drives SphereWorld and its
+    shader (constructor scene, 8-thread RenderThread interleave, UpdateSpheres uniform
+    uploads): frames equal the golden hashes (tests/native/cpp_api_check.cpp)."""
+    exe = tmp_path / "cpp_api_check"
+    lib_dir = os.path.join(ROOT, "sfml-software-raytracer_amd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "native", "cpp_api_check.cpp"), "-L", lib_dir,
+                    "-lsfrt", f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath-link,/opt/rocm/lib",
+                    "-lpthread", "-o", str(exe)], check=True, capture_output=True)
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+    want_s = golden["frames"]["c2_1920x1080_default10@0,0"]["fnv1a64"]
+    want_g = golden["glsl"]["default@320x180"]["fnv1a64"]
+    r = subprocess.run([str(exe), os.path.join(lib_dir, "assets"), want_s, want_g],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "failures=0" in r.stdout, r.stdout + r.stderr
+
+
 def test_pipelined_frames_match_update_image(world, floor):
     """Display path: two frames in flight, camera changing per frame."""
     import sfrt
