@@ -326,6 +326,20 @@ def main() -> None:
             "n_gpus": 1, "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
             "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4)}
         w2.close()
+        # BASELINE config 3 with "all textures": every reference texture resident, one
+        # per sphere (the per-sphere texture extension; the main line is textures[0]).
+        w3 = sfrt.World(local_rank)
+        for slot, (rgba, tw, th) in enumerate(scenes.load_all_textures()):
+            w3.load_texture(rgba, tw, th, slot=slot)
+        w3.set_scene(scene, WIDTH, height)
+        w3.set_sphere_textures(scenes.all_texture_slots(scene.spheres.shape[0]))
+        pipe3 = BandPipeline(0, 1, height, pitch, "cuda")
+        wall3, k3 = time_frames(w3, pipe3, pitch, args.steps, args.warmup, stream)
+        result["also"]["3840x2160_lcg64_all_textures"] = {
+            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall3 / 1e6, 2),
+            "fps": round(args.steps / wall3, 2), "kernel_ms": round(k3, 4)}
+        w3.close()
+        del pipe3
         if not args.no_cpu_baseline:
             torch.cuda.synchronize()
             gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()

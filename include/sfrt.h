@@ -89,6 +89,12 @@ SFRT_API int sfrt_world_add_sphere(sfrt_world* w, float x, float y, float z, flo
 /* Replace the sphere list verbatim (caller order = the order the march visits). */
 SFRT_API int sfrt_world_set_spheres(sfrt_world* w, const sfrt_sphere* spheres, int count);
 SFRT_API int sfrt_world_get_spheres(const sfrt_world* w, sfrt_sphere* out, int capacity, int* count);
+/* Extension ("all textures"): a texture slot per sphere, in the
+ * current sphere order (count == number of spheres); slots travel with their spheres
+ * through AddSphere / UpdateSpheres.  Default 0 = textures[0] everywhere = the
+ * reference (SphereWorld.cpp:376-377 samples textures[0] only). */
+SFRT_API int sfrt_world_set_sphere_textures(sfrt_world* w, const int32_t* slots, int count);
+SFRT_API int sfrt_world_get_sphere_textures(sfrt_world* w, int32_t* out, int capacity, int* count);
 /* UpdateSpheres sort part (SphereWorld.cpp:199-212): stable by |c - cam.pos| + r. */
 SFRT_API int sfrt_world_update_spheres(sfrt_world* w);
 

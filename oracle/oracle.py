@@ -30,6 +30,9 @@ class OracleScene(ctypes.Structure):
         ("spheres", ctypes.POINTER(OracleSphere)), ("sphere_count", ctypes.c_int),
         ("texture", ctypes.POINTER(ctypes.c_uint8)),
         ("tex_w", ctypes.c_int), ("tex_h", ctypes.c_int),
+        ("sphere_tex", ctypes.POINTER(ctypes.c_int32)),
+        ("textures", ctypes.POINTER(ctypes.c_uint8) * 10),
+        ("tex_ws", ctypes.c_int * 10), ("tex_hs", ctypes.c_int * 10),
     ]
 
 
@@ -82,7 +85,10 @@ class Oracle:
     """One scene + texture bound for repeated oracle calls."""
 
     def __init__(self, width, height, spheres, texture, tex_w, tex_h, cam_pos=(0, 0, 0),
-                 rotation=0.0, hrotation=0.0, fov_h=None, fov_v=None):
+                 rotation=0.0, hrotation=0.0, fov_h=None, fov_v=None, sphere_tex=None,
+                 textures=None):
+        """sphere_tex / textures: the per-sphere texture extension (slot per sphere;
+        {slot: (rgba, w, h)} for slots 1..9); None = the reference (slot 0 only)."""
         sph = np.ascontiguousarray(np.asarray(spheres, dtype=np.float32).reshape(-1, 4))
         self._sph = sph
         self._tex = np.ascontiguousarray(np.asarray(texture, dtype=np.uint8).ravel())
@@ -97,6 +103,17 @@ class Oracle:
         sc.sphere_count = sph.shape[0]
         sc.texture = self._tex.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
         sc.tex_w, sc.tex_h = int(tex_w), int(tex_h)
+        self._keep = []
+        if sphere_tex is not None:
+            st = np.ascontiguousarray(np.asarray(sphere_tex, dtype=np.int32))
+            assert st.size == sph.shape[0]
+            self._keep.append(st)
+            sc.sphere_tex = st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        for k, (rgba, w, h) in (textures or {}).items():
+            buf = np.ascontiguousarray(np.asarray(rgba, dtype=np.uint8).ravel())
+            self._keep.append(buf)
+            sc.textures[k] = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+            sc.tex_ws[k], sc.tex_hs[k] = int(w), int(h)
         self.scene = sc
 
     @classmethod

@@ -106,12 +106,16 @@ static uint32_t trace_pixel(const oracle_scene* sc, v3 dir, oracle_pixel_dump* d
   float ycoord = (asinf(vnormalize(vsub(pos, dc)).y) / O_PI + 0.5f); /* :374 */
   float len = vlength(vsub(pos, cam));
   float brightness = 3.0f / (len < 3.0f ? 3.0f : len);              /* :375 */
-  /* :376-377: getPixel((unsigned)(fmodf(..)*texsize.x), (unsigned)(..)) */
-  float fx = fmodf(xcoord * 4 * d->radius, 1.0f) * (float)(unsigned)sc->tex_w;
-  float fy = fmodf(ycoord * 2 * d->radius, 1.0f) * (float)(unsigned)sc->tex_h;
+  /* :376-377: getPixel((unsigned)(fmodf(..)*texsize.x), (unsigned)(..)); the
+   * texture is textures[0] unless the per-sphere extension names another slot */
+  const int slot = sc->sphere_tex ? sc->sphere_tex[draw] : 0;
+  const uint8_t* tex = slot ? sc->textures[slot] : sc->texture;
+  const int tw = slot ? sc->tex_ws[slot] : sc->tex_w, th = slot ? sc->tex_hs[slot] : sc->tex_h;
+  float fx = fmodf(xcoord * 4 * d->radius, 1.0f) * (float)(unsigned)tw;
+  float fy = fmodf(ycoord * 2 * d->radius, 1.0f) * (float)(unsigned)th;
   unsigned tx = (unsigned)(int64_t)fx; /* x86-64 g++: cvttss2si to 64-bit, low 32 bits */
   unsigned ty = (unsigned)(int64_t)fy;
-  const uint8_t* px = sc->texture + ((size_t)(tx + ty * (unsigned)sc->tex_w)) * 4;
+  const uint8_t* px = tex + ((size_t)(tx + ty * (unsigned)tw)) * 4;
   uint8_t r = px[0], g = px[1], b = px[2], a = px[3];
   r = (uint8_t)(int)(r * brightness);                                 /* :378 */
   g = (uint8_t)(int)(g * brightness);                                 /* :379 */
@@ -149,6 +153,12 @@ int oracle_scene_valid(const oracle_scene* sc) {
   if (!sc || sc->width <= 0 || sc->height <= 0) return 0;
   if (sc->sphere_count <= 0 || !sc->spheres) return 0;  /* spheres.at(0) throws */
   if (!sc->texture || sc->tex_w <= 0 || sc->tex_h <= 0) return 0;
+  if (sc->sphere_tex)
+    for (int i = 0; i < sc->sphere_count; i++) {
+      const int k = sc->sphere_tex[i];
+      if (k < 0 || k >= 10 || (k && (!sc->textures[k] || sc->tex_ws[k] <= 0 || sc->tex_hs[k] <= 0)))
+        return 0;
+    }
   return 1;
 }
 

@@ -21,6 +21,12 @@ typedef struct {
   int sphere_count;
   const uint8_t* texture;        /* RGBA8, tex_w * tex_h * 4 */
   int tex_w, tex_h;
+  /* Extension ("all textures"): a texture slot per sphere,
+   * in sphere order; NULL = slot 0 (`texture`) for every sphere, which is the
+   * reference.  Slots 1..9 are textures[k] with tex_ws[k] x tex_hs[k] texels. */
+  const int32_t* sphere_tex;
+  const uint8_t* textures[10];
+  int tex_ws[10], tex_hs[10];
 } oracle_scene;
 
 typedef struct {

@@ -30,7 +30,8 @@ struct SphereRec {
   float cx, cy, cz, r;
   float s_pass;    // exact pass threshold: r - sqrtf(s) > 0.01f  <=>  s < s_pass
   float atan_c;    // atan2f(cz, cx), the centre term of VAngleXZ (SphereWorld.cpp:326)
-  float pad0, pad1;
+  uint32_t tex_off;  // this sphere's texture (textures[0], or its extension slot) in the atlas
+  uint32_t tex_wh;   // its width | height << 16
 };
 
 struct FrameRec {
@@ -45,14 +46,12 @@ struct FrameRec {
   int sub_w;                        // columns in the subset
   int sub_row0, sub_rows;           // subset rows rendered by this launch
   int tiles_x;                      // ceil(sub_w / 8)
-  int tex_w, tex_h;
-  float tex_wf, tex_hf;             // (float)texsize.x / .y (SphereWorld.cpp:376-377)
   int cull;                         // 1: per-wave cone culling (default), 0: every sphere
   float cull_margin;                // absolute inflation of every sphere in the cone test
   int variant;                      // kernel variant for tuning A/B (0 = default)
   long long out_pitch;              // output pitch in pixels
   uint32_t* out;                    // pixel (a, b) -> out[(b - sub_row0) * out_pitch + a]
-  const uint32_t* tex;              // RGBA8 texels
+  const uint32_t* tex;              // RGBA8 texture atlas (every loaded slot, back to back)
   const SphereRec* spheres;         // device copy (used when n > kInlineSpheres)
   int* status;                      // device word: bit 0 = march guard hit, bit 1 = bad texel
 };

@@ -56,10 +56,13 @@ bool sphere_ok(const sfrt_sphere& s) {
 }
 
 // Stable insertion by |c - cam| + r, inserted after equal keys (SphereWorld.cpp:201-212).
-void sort_spheres(std::vector<sfrt_sphere>& spheres, V3 cam) {
+// Returns the permutation (new position -> old index).
+std::vector<size_t> sort_spheres(std::vector<sfrt_sphere>& spheres, V3 cam) {
   std::vector<sfrt_sphere> temp = spheres;
+  std::vector<size_t> order;
   spheres.clear();
-  for (const sfrt_sphere& t : temp) {
+  for (size_t k = 0; k < temp.size(); k++) {
+    const sfrt_sphere& t = temp[k];
     const float dist = vlength(vsub(center(t), cam)) + t.radius;
     size_t ins = 0;
     for (size_t j = 0; j < spheres.size(); j++) {
@@ -67,7 +70,16 @@ void sort_spheres(std::vector<sfrt_sphere>& spheres, V3 cam) {
       ins++;
     }
     spheres.insert(spheres.begin() + (long)ins, t);
+    order.insert(order.begin() + (long)ins, k);
   }
+  return order;
+}
+
+template <class T>
+void permute(std::vector<T>& v, const std::vector<size_t>& order) {
+  std::vector<T> out(order.size());
+  for (size_t i = 0; i < order.size(); i++) out[i] = v[order[i]];
+  v.swap(out);
 }
 
 bool passes(float r, float s) { return r - std::sqrt(s) > 0.01f; }  // SphereWorld.cpp:365-366
@@ -115,14 +127,18 @@ struct sfrt_world {
   int height = 180;  // SphereWorld.h:51
   sfrt_camera cam{};
   std::vector<sfrt_sphere> spheres;
+  // Per-sphere texture slot, parallel to `spheres` (the "all textures" extension
+  // of SURVEY 8d config 3; 0 everywhere = the reference, textures[0]).
+  std::vector<int32_t> sphere_tex;
   std::vector<uint8_t> tex_host[SFRT_TEXTURE_SLOTS];
   int tex_w[SFRT_TEXTURE_SLOTS] = {};
   int tex_h[SFRT_TEXTURE_SLOTS] = {};
+  uint32_t tex_off[SFRT_TEXTURE_SLOTS] = {};  // texel offset of each slot in the atlas
   int cull = 1;
   int variant = 0;
   // --- device resources ---
   hipStream_t stream = nullptr;
-  uint32_t* d_tex = nullptr;  // textures[0] on the device
+  uint32_t* d_tex = nullptr;  // texture atlas: every loaded slot, back to back
   size_t d_tex_texels = 0;
   int* d_status = nullptr;
   static constexpr int kRing = 8;
@@ -172,6 +188,8 @@ struct sfrt_world {
     if (spheres.empty()) return SFRT_E_EMPTY;
     if ((int)spheres.size() > SFRT_MAX_SPHERES) return SFRT_E_TOO_MANY;
     if (tex_host[0].empty() || !d_tex) return SFRT_E_NO_TEXTURE;
+    for (int32_t k : sphere_tex)
+      if (tex_host[k].empty()) return SFRT_E_NO_TEXTURE;
     if (width <= 0 || height <= 0) return SFRT_E_INVALID;
     return SFRT_OK;
   }
@@ -212,10 +230,6 @@ struct sfrt_world {
     f.n = (int)spheres.size();
     f.width = width;
     f.height = height;
-    f.tex_w = tex_w[0];
-    f.tex_h = tex_h[0];
-    f.tex_wf = (float)(unsigned)tex_w[0];
-    f.tex_hf = (float)(unsigned)tex_h[0];
     f.cull = cull;
     f.variant = variant;
     // Culling margin (sphere_trace.hip, cull_mask).  A march step
@@ -241,7 +255,9 @@ struct sfrt_world {
       r.cx = s.x; r.cy = s.y; r.cz = s.z; r.r = s.radius;
       r.s_pass = pass_threshold(s.radius);
       r.atan_c = sfrt_math::atan2f(s.z, s.x);  // == libm atan2f (tests/test_math_exhaustive.py)
-      r.pad0 = r.pad1 = 0.0f;
+      const int k = sphere_tex[i];
+      r.tex_off = tex_off[k];
+      r.tex_wh = (uint32_t)tex_w[k] | ((uint32_t)tex_h[k] << 16);
     }
   }
 
@@ -343,23 +359,34 @@ int sfrt_world_get_camera(const sfrt_world* w, sfrt_camera* cam) {
 
 int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int tex_w, int tex_h) {
   if (!w || !rgba || slot < 0 || slot >= SFRT_TEXTURE_SLOTS || tex_w <= 0 || tex_h <= 0 ||
-      (int64_t)tex_w * tex_h > (1 << 28))
+      tex_w > 0xffff || tex_h > 0xffff || (int64_t)tex_w * tex_h > (1 << 28))
     return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(w->mu);
   const size_t bytes = (size_t)tex_w * tex_h * 4;
   w->tex_host[slot].assign(rgba, rgba + bytes);
   w->tex_w[slot] = tex_w;
   w->tex_h[slot] = tex_h;
-  if (slot != 0) return SFRT_OK;  // only textures[0] is sampled (SphereWorld.cpp:376-377)
+  // Rebuild the device atlas: textures[0] (SphereWorld.cpp:376-377) first, then
+  // the extension slots.  Draws on any stream may still read the old atlas.
+  size_t total = 0;
+  for (int k = 0; k < SFRT_TEXTURE_SLOTS; k++) {
+    w->tex_off[k] = (uint32_t)total;
+    total += (size_t)w->tex_w[k] * w->tex_h[k];
+  }
+  if (total > 0xffffffffull) return SFRT_E_INVALID;
   DeviceGuard g(w->device);
-  HIP_TRY(hipStreamSynchronize(w->stream));
-  if (w->d_tex_texels < (size_t)tex_w * tex_h) {
+  HIP_TRY(hipDeviceSynchronize());
+  if (w->d_tex_texels < total) {
     (void)hipFree(w->d_tex);
     w->d_tex = nullptr;
-    HIP_TRY(hipMalloc(&w->d_tex, bytes));
-    w->d_tex_texels = (size_t)tex_w * tex_h;
+    w->d_tex_texels = 0;
+    HIP_TRY(hipMalloc(&w->d_tex, total * 4));
+    w->d_tex_texels = total;
   }
-  HIP_TRY(hipMemcpy(w->d_tex, rgba, bytes, hipMemcpyHostToDevice));
+  for (int k = 0; k < SFRT_TEXTURE_SLOTS; k++)
+    if (!w->tex_host[k].empty())
+      HIP_TRY(hipMemcpy(w->d_tex + w->tex_off[k], w->tex_host[k].data(), w->tex_host[k].size(),
+                        hipMemcpyHostToDevice));
   return SFRT_OK;
 }
 
@@ -368,18 +395,21 @@ int sfrt_world_add_sphere(sfrt_world* w, float x, float y, float z, float radius
   if (!w || !sphere_ok(add)) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(w->mu);
   std::vector<sfrt_sphere>& s = w->spheres;
+  std::vector<int32_t>& st = w->sphere_tex;
   s.push_back(add);
+  st.push_back(0);
   // SphereWorld.cpp:180-188: drop every sphere contained in another one.
   for (int i = 0; i < (int)s.size(); i++) {
     for (int j = 0; j < (int)s.size(); j++) {
       if (i != j && vlength(vsub(center(s[i]), center(s[j]))) + s[i].radius <= s[j].radius) {
         s.erase(s.begin() + i);
+        st.erase(st.begin() + i);
         i--;
         break;
       }
     }
   }
-  sort_spheres(s, {w->cam.pos[0], w->cam.pos[1], w->cam.pos[2]});
+  permute(st, sort_spheres(s, {w->cam.pos[0], w->cam.pos[1], w->cam.pos[2]}));
   if ((int)s.size() > SFRT_MAX_SPHERES) return SFRT_E_TOO_MANY;
   return SFRT_OK;
 }
@@ -391,6 +421,28 @@ int sfrt_world_set_spheres(sfrt_world* w, const sfrt_sphere* spheres, int count)
     if (!sphere_ok(spheres[i])) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(w->mu);
   w->spheres.assign(spheres, spheres + count);
+  w->sphere_tex.assign((size_t)count, 0);
+  return SFRT_OK;
+}
+
+int sfrt_world_set_sphere_textures(sfrt_world* w, const int32_t* slots, int count) {
+  if (!w || count < 0 || (count > 0 && !slots)) return SFRT_E_INVALID;
+  for (int i = 0; i < count; i++)
+    if (slots[i] < 0 || slots[i] >= SFRT_TEXTURE_SLOTS) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  if ((size_t)count != w->spheres.size()) return SFRT_E_INVALID;
+  w->sphere_tex.assign(slots, slots + count);
+  return SFRT_OK;
+}
+
+int sfrt_world_get_sphere_textures(sfrt_world* w, int32_t* out, int capacity, int* count) {
+  if (!w || !count) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  *count = (int)w->sphere_tex.size();
+  if (out) {
+    const int n = capacity < *count ? capacity : *count;
+    std::memcpy(out, w->sphere_tex.data(), sizeof(int32_t) * (size_t)(n > 0 ? n : 0));
+  }
   return SFRT_OK;
 }
 
@@ -407,7 +459,7 @@ int sfrt_world_get_spheres(const sfrt_world* w, sfrt_sphere* out, int capacity, 
 int sfrt_world_update_spheres(sfrt_world* w) {
   if (!w) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(w->mu);
-  sort_spheres(w->spheres, {w->cam.pos[0], w->cam.pos[1], w->cam.pos[2]});
+  permute(w->sphere_tex, sort_spheres(w->spheres, {w->cam.pos[0], w->cam.pos[1], w->cam.pos[2]}));
   return SFRT_OK;
 }
 

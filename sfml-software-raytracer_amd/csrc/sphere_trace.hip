@@ -59,16 +59,18 @@ __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d,
   const float bl = sqrt_cr((bx * bx + by * by) + bz * bz);
   const float brightness = 3.0f / (bl < 3.0f ? 3.0f : bl);
   // fmodf(v, 1.0f) == v - truncf(v) exactly for every binary32 v (NaN/inf -> NaN).
+  // texsize of textures[0] (or of the sphere's extension slot), (float)(unsigned) as :376
+  const uint32_t tw = d.tex_wh & 0xffffu, th = d.tex_wh >> 16;
   float u = xcoord * 4.0f * d.r;
-  u = (u - __builtin_truncf(u)) * f.tex_wf;
+  u = (u - __builtin_truncf(u)) * (float)tw;
   float w = ycoord * 2.0f * d.r;
-  w = (w - __builtin_truncf(w)) * f.tex_hf;
+  w = (w - __builtin_truncf(w)) * (float)th;
   // float -> unsigned: v_cvt_u32_f32 (NaN -> 0), as x86's cvttss2si for [0, 2^31).
   const uint32_t tx = __float2uint_rz(u), ty = __float2uint_rz(w);
-  const uint32_t idx = tx + ty * (uint32_t)f.tex_w;
+  const uint32_t idx = tx + ty * tw;
   uint32_t texel = 0;
-  if (idx < (uint32_t)(f.tex_w * f.tex_h)) {
-    texel = f.tex[idx];
+  if (idx < tw * th) {
+    texel = f.tex[d.tex_off + idx];
   } else {
     atomicOr(f.status, 2);  // the reference would read outside the image here
   }

@@ -124,6 +124,32 @@ def load_floor() -> tuple[np.ndarray, int, int]:
     return data, 128, 128
 
 
+# SURVEY 8d config 3, "all textures": every texture the reference ships, one slot each
+# (slot 0 = Floor.png = textures[0]); the extension samples slot (i % 6) for the
+# sphere at sorted position i.  Decoded RGBA8 assets (tools/make_assets.py).
+ALL_TEXTURES = ["floor_128x128", "Wall", "Ceiling", "Block", "dynamic", "Projectile"]
+
+
+def load_all_textures() -> list:
+    out = []
+    for name in ALL_TEXTURES:
+        if name == "floor_128x128":
+            out.append(load_floor())
+            continue
+        path = os.path.join(HERE, "assets", f"{name}.rgba")
+        with open(path + ".shape") as f:
+            w, h = (int(v) for v in f.read().split())
+        data = np.fromfile(path, dtype=np.uint8)
+        if data.size != w * h * 4:
+            raise RuntimeError(f"{path}: expected {w * h * 4} bytes, got {data.size}")
+        out.append((data, w, h))
+    return out
+
+
+def all_texture_slots(n: int) -> np.ndarray:
+    return (np.arange(n) % len(ALL_TEXTURES)).astype(np.int32)
+
+
 # Workloads named by BASELINE.json's configs; (width, height, scene, poses).
 CONFIGS = {
     "c1_320x240_one_sphere": (320, 240, "one_sphere", [(0.0, 0.0)]),

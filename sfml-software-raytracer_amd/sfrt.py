@@ -30,6 +30,7 @@ ABI_SYMBOLS = (
     "sfrt_world_create", "sfrt_world_destroy", "sfrt_world_set_size", "sfrt_world_get_size",
     "sfrt_world_set_camera", "sfrt_world_get_camera", "sfrt_world_load_texture",
     "sfrt_world_add_sphere", "sfrt_world_set_spheres", "sfrt_world_get_spheres",
+    "sfrt_world_set_sphere_textures", "sfrt_world_get_sphere_textures",
     "sfrt_world_update_spheres", "sfrt_world_update_image", "sfrt_world_render_band",
     "sfrt_world_check", "sfrt_world_trace_points", "sfrt_world_set_option",
     "sfrt_world_submit_frame", "sfrt_world_wait_frame", "sfrt_host_alloc", "sfrt_host_free",
@@ -103,6 +104,8 @@ def lib() -> ctypes.CDLL:
         "sfrt_world_add_sphere": ([W, c_float, c_float, c_float, c_float], c_int),
         "sfrt_world_set_spheres": ([W, vp, c_int], c_int),
         "sfrt_world_get_spheres": ([W, vp, c_int, P(c_int)], c_int),
+        "sfrt_world_set_sphere_textures": ([W, vp, c_int], c_int),
+        "sfrt_world_get_sphere_textures": ([W, vp, c_int, P(c_int)], c_int),
         "sfrt_world_update_spheres": ([W], c_int),
         "sfrt_world_update_image": ([W, vp, c_int, c_int, c_int, c_int], c_int),
         "sfrt_world_render_band": ([W, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
@@ -276,6 +279,22 @@ class World:
         out = np.zeros((n.value, 4), dtype=np.float32)
         _check(lib().sfrt_world_get_spheres(self._h, out.ctypes.data, n.value, ctypes.byref(n)),
                "get_spheres")
+        return out
+
+    def set_sphere_textures(self, slots) -> None:
+        """Texture slot per sphere (current order): the "all textures" extension."""
+        a = np.ascontiguousarray(np.asarray(slots, dtype=np.int32).ravel())
+        _check(lib().sfrt_world_set_sphere_textures(self._h, a.ctypes.data, a.size),
+               "set_sphere_textures")
+
+    @property
+    def sphere_textures(self) -> np.ndarray:
+        n = ctypes.c_int()
+        _check(lib().sfrt_world_get_sphere_textures(self._h, None, 0, ctypes.byref(n)),
+               "get_sphere_textures")
+        out = np.zeros(n.value, dtype=np.int32)
+        _check(lib().sfrt_world_get_sphere_textures(self._h, out.ctypes.data, n.value,
+                                                    ctypes.byref(n)), "get_sphere_textures")
         return out
 
     def update_spheres(self) -> None:

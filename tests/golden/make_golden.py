@@ -1,6 +1,6 @@
 """Generate tests/golden/ from the CPU restatement (oracle/).
 
-    python tests/golden/make_golden.py [--only-glsl]
+    python tests/golden/make_golden.py [--only=glsl] [--only=all_textures]
 
 Writes golden.json: per (config, pose) the frame's FNV-1a-64 and SHA-256,
 per-row FNV-1a-64 for frames up to 4K, the march-iteration statistics, and
@@ -53,12 +53,29 @@ def glsl_section(threads):
     return sec
 
 
+def all_textures_section(threads):
+    """Per-sphere texture extension, oracle/sphereworld_oracle.c."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_all_textures import CASES, key, tex_oracle
+    sec = {}
+    for case in CASES:
+        frame = tex_oracle(*case).render(threads)
+        sec[key(*case)] = {"fnv1a64": oracle.fnv1a64(frame)}
+        print("all_textures", key(*case), sec[key(*case)]["fnv1a64"], flush=True)
+    return sec
+
+
+SECTIONS = {"glsl": glsl_section, "all_textures": all_textures_section}
+
+
 def main():
     oracle.build()
-    if "--only-glsl" in sys.argv:
+    only = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--only=")]
+    if only:
         path = os.path.join(HERE, "golden.json")
         out = json.load(open(path))
-        out["glsl"] = glsl_section(os.cpu_count() or 1)
+        for name in only:
+            out[name] = SECTIONS[name](os.cpu_count() or 1)
         with open(path, "w") as f:
             json.dump(out, f, indent=0, sort_keys=True)
         return
@@ -105,7 +122,8 @@ def main():
                                         "rotation": r, "hrotation": hr,
                                         "fnv1a64": oracle.fnv1a64(frame)}
         print("voxel", case_key(case), out["voxel"][case_key(case)]["fnv1a64"], flush=True)
-    out["glsl"] = glsl_section(threads)
+    for name, fn in SECTIONS.items():
+        out[name] = fn(threads)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(out, f, indent=0, sort_keys=True)
 

@@ -214,10 +214,45 @@ def _far_balls(w, h):
     return u
 
 
+def _no_walls(w, h):
+    u = gs.random_uniforms(7, 1, 1, 6, w, h)
+    u["spheres"][:-1] = u["spheres"][1:].copy()     # drop the wall: sphereCount 0
+    u["uvs"][:-1] = u["uvs"][1:].copy()
+    u["lights"][:-1] = u["lights"][1:].copy()
+    u["sphere_count"], u["all_spheres_count"] = 0, int(u["all_spheres_count"]) - 1
+    return u
+
+
+def _walls_only(w, h):
+    return gs.random_uniforms(8, 9, 0, 0, w, h)
+
+
+def _empty(w, h):
+    u = gs.random_uniforms(9, 1, 0, 0, w, h)
+    u["sphere_count"] = u["all_spheres_count"] = 0
+    return u
+
+
+def _camera_outside(w, h):
+    u = gs.default_uniforms(w, h, 0.2, 0.1)
+    u["campos"] = (30.0, 2.0, -25.0)
+    return u
+
+
+EDGE = [_negzero_cam, _far_balls, _no_walls, _walls_only, _empty, _camera_outside]
+
+
+@pytest.mark.parametrize("make", EDGE, ids=[m.__name__.strip("_") for m in EDGE])
+def test_oracle_edge_uniforms_run(floor, make):
+    """Degenerate uniform blocks the shader accepts render without hitting the march cap."""
+    o = oracle.GlslOracle(make(96, 54), *floor)
+    assert o.render(96, 54, host_threads()).size == 96 * 54 * 4
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("make", [_negzero_cam, _far_balls], ids=["negzero_cam", "far_balls"])
+@pytest.mark.parametrize("make", EDGE, ids=[m.__name__.strip("_") for m in EDGE])
 def test_gpu_edge_uniforms(shader, floor, make):
-    w, h = 320, 180
+    w, h = 320, 181
     u = make(w, h)
     got = draw(shader, u, w, h)
     want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
