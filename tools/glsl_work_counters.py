@@ -1,5 +1,7 @@
+"""Per-wave work counters of the GLSL kernel (instrumented build from tools/instrument_glsl.py):
+wall iterations, march steps, dominance tests / ball bodies, shadow visits.  GPU only."""
 import ctypes, json, os, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
 import torch, glsl_scenes as gs, scenes, sfrt
 L = sfrt.lib()
