@@ -70,20 +70,6 @@ int upload_texture(DevTex& t, const uint8_t* rgba, int w, int h) {
   return SFRT_OK;
 }
 
-template <typename T>
-int upload_vector(T*& d, size_t& cap, const std::vector<T>& v, hipStream_t s) {
-  if (v.empty()) return SFRT_OK;
-  if (cap < v.size()) {
-    (void)hipFree(d);
-    d = nullptr;
-    HIP_TRY(hipMalloc(&d, sizeof(T) * v.size()));
-    cap = v.size();
-  }
-  // pageable source: staged by the runtime before the call returns
-  HIP_TRY(hipMemcpyAsync(d, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s));
-  return SFRT_OK;
-}
-
 }  // namespace
 
 struct sfrt_voxel {
@@ -104,15 +90,20 @@ struct sfrt_voxel {
   int16_t* d_blocks = nullptr;
   size_t d_blocks_cap = 0;
   bool blocks_dirty = true;
-  // per-frame arrays (stream-ordered reuse: every upload precedes its kernel on `stream`)
-  float* d_col = nullptr;
-  size_t d_col_cap = 0;
-  float* d_row = nullptr;
-  size_t d_row_cap = 0;
-  sfrt::VoxDyn* d_dyn = nullptr;
-  size_t d_dyn_cap = 0;
-  sfrt::VoxLight* d_lights = nullptr;
-  size_t d_lights_cap = 0;
+  // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
+  // with pinned staging and the event of the last launch that read it, so
+  // launches on different streams never see a table overwritten under them.
+  struct TableSlot {
+    void* d = nullptr;
+    void* h = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  };
+  static constexpr int kSlots = 4;
+  TableSlot slots[kSlots];
+  int next_slot = 0;
+  int cur_slot = -1;
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
@@ -123,11 +114,13 @@ struct sfrt_voxel {
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& t : tex) (void)hipFree(t.d);
     for (auto& t : dyn_tex) (void)hipFree(t.d);
+    (void)hipDeviceSynchronize();
     (void)hipFree(d_blocks);
-    (void)hipFree(d_col);
-    (void)hipFree(d_row);
-    (void)hipFree(d_dyn);
-    (void)hipFree(d_lights);
+    for (auto& t : slots) {
+      (void)hipFree(t.d);
+      (void)hipHostFree(t.h);
+      if (t.ev) (void)hipEventDestroy(t.ev);
+    }
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
     if (stream) (void)hipStreamDestroy(stream);
@@ -184,24 +177,50 @@ struct sfrt_voxel {
       const sfrt_light& L = lights[k];
       vl[k] = {L.pos[0], L.pos[1], L.pos[2], L.intensity, L.r, L.g, L.b, L.shadows, 0};
     }
-    int rc;
-    if ((rc = upload_vector(d_col, d_col_cap, col, s)) || (rc = upload_vector(d_row, d_row_cap, row, s)) ||
-        (rc = upload_vector(d_dyn, d_dyn_cap, vd, s)) ||
-        (rc = upload_vector(d_lights, d_lights_cap, vl, s)))
-      return rc;
-    if (blocks_dirty) {
+    // one blob per launch: col | row | dyn | lights, 16-byte aligned parts
+    auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const size_t b_col = up16(col.size() * sizeof(float)), b_row = up16(row.size() * sizeof(float)),
+                 b_dyn = up16(vd.size() * sizeof(sfrt::VoxDyn)),
+                 b_lit = up16(vl.size() * sizeof(sfrt::VoxLight));
+    const size_t bytes = b_col + b_row + b_dyn + b_lit + 16;
+    TableSlot& t = slots[next_slot];
+    if (t.pending) HIP_TRY(hipEventSynchronize(t.ev));
+    t.pending = false;
+    if (!t.ev) HIP_TRY(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
+    if (t.cap < bytes) {
+      (void)hipFree(t.d);
+      (void)hipHostFree(t.h);
+      t.d = t.h = nullptr;
+      t.cap = 0;
+      HIP_TRY(hipMalloc(&t.d, bytes));
+      HIP_TRY(hipHostMalloc(&t.h, bytes, hipHostMallocDefault));
+      t.cap = bytes;
+    }
+    uint8_t* h = (uint8_t*)t.h;
+    std::memcpy(h, col.data(), col.size() * sizeof(float));
+    std::memcpy(h + b_col, row.data(), row.size() * sizeof(float));
+    if (!vd.empty()) std::memcpy(h + b_col + b_row, vd.data(), vd.size() * sizeof(sfrt::VoxDyn));
+    if (!vl.empty())
+      std::memcpy(h + b_col + b_row + b_dyn, vl.data(), vl.size() * sizeof(sfrt::VoxLight));
+    HIP_TRY(hipMemcpyAsync(t.d, t.h, bytes, hipMemcpyHostToDevice, s));
+    cur_slot = next_slot;
+    next_slot = (next_slot + 1) % kSlots;
+    uint8_t* d = (uint8_t*)t.d;
+    if (blocks_dirty) {  // rare: launches on any stream may still read the old grid
+      HIP_TRY(hipDeviceSynchronize());
       if (d_blocks_cap < blocks.size()) {
         (void)hipFree(d_blocks);
         d_blocks = nullptr;
+        d_blocks_cap = 0;
         HIP_TRY(hipMalloc(&d_blocks, blocks.size() * sizeof(int16_t)));
         d_blocks_cap = blocks.size();
       }
-      HIP_TRY(hipMemcpyAsync(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
-                             hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpy(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
+                        hipMemcpyHostToDevice));
       blocks_dirty = false;
     }
-    f.col = d_col;
-    f.row = d_row;
+    f.col = (const float*)d;
+    f.row = (const float*)(d + b_col);
     f.blocks = d_blocks;
     f.nx = nx; f.ny = ny; f.nz = nz;
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
@@ -209,11 +228,19 @@ struct sfrt_voxel {
       f.dyn_tex[k] = {dyn_tex[k].d, dyn_tex[k].w, dyn_tex[k].h};
       f.colors[k] = colors[k];
     }
-    f.dyn = d_dyn;
+    f.dyn = (const sfrt::VoxDyn*)(d + b_col + b_row);
     f.ndyn = (int)dyn.size();
-    f.lights = d_lights;
+    f.lights = (const sfrt::VoxLight*)(d + b_col + b_row + b_dyn);
     f.nlights = (int)lights.size();
     f.status = d_status;
+    return SFRT_OK;
+  }
+
+  // Marks the current table slot busy until the work queued on s completes.
+  int launched(hipStream_t s) {
+    TableSlot& t = slots[cur_slot];
+    HIP_TRY(hipEventRecord(t.ev, s));
+    t.pending = true;
     return SFRT_OK;
   }
 
@@ -301,7 +328,7 @@ int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w,
   if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   DeviceGuard g(v->device);
-  HIP_TRY(hipStreamSynchronize(v->stream));
+  HIP_TRY(hipDeviceSynchronize());  // launches on any stream may read it
   return upload_texture(v->tex[slot], rgba, w, h);
 }
 
@@ -309,7 +336,7 @@ int sfrt_voxel_load_dyn_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, in
   if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   DeviceGuard g(v->device);
-  HIP_TRY(hipStreamSynchronize(v->stream));
+  HIP_TRY(hipDeviceSynchronize());
   return upload_texture(v->dyn_tex[slot], rgba, w, h);
 }
 
@@ -362,6 +389,7 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   f.out = v->d_frame;
   f.out_pitch = sub_w;
   if (sfrt::launch_voxel(f, v->stream)) return SFRT_E_HIP;
+  if ((rc = v->launched(v->stream))) return rc;
   std::vector<uint32_t> stage(px);
   HIP_TRY(hipMemcpyAsync(stage.data(), v->d_frame, px * 4, hipMemcpyDeviceToHost, v->stream));
   rc = v->read_status(v->stream);
@@ -392,7 +420,8 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   f.sub_rows = rows;
   f.out = (uint32_t*)dev_pixels;
   f.out_pitch = pitch_bytes / 4;
-  return sfrt::launch_voxel(f, s) ? SFRT_E_HIP : SFRT_OK;
+  if (sfrt::launch_voxel(f, s)) return SFRT_E_HIP;
+  return v->launched(s);
 }
 
 int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream) {

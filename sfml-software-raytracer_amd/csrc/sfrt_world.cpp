@@ -141,10 +141,18 @@ struct sfrt_world {
   uint32_t* d_tex = nullptr;  // texture atlas: every loaded slot, back to back
   size_t d_tex_texels = 0;
   int* d_status = nullptr;
+  // Device copies of the sphere records for launches that read them from memory
+  // (> 64 spheres, trace_points): a ring of slots, each with pinned staging and
+  // the event of the last launch that read it, so a slot is never overwritten
+  // while a launch on any stream may still read it.
   static constexpr int kRing = 8;
   sfrt::SphereRec* d_spheres[kRing] = {};
+  sfrt::SphereRec* h_spheres[kRing] = {};
+  hipEvent_t spheres_ev[kRing] = {};
+  bool spheres_pending[kRing] = {};
   int d_spheres_cap = 0;
   int ring = 0;
+  int staged = -1;  // slot staged for the launch being prepared, or -1
   uint32_t* d_frame = nullptr;  // compact subset buffer for the host path
   size_t d_frame_px = 0;
   uint32_t* h_stage = nullptr;  // pinned D2H staging
@@ -178,7 +186,12 @@ struct sfrt_world {
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     (void)hipFree(d_tex);
     (void)hipFree(d_status);
-    for (auto* p : d_spheres) (void)hipFree(p);
+    (void)hipDeviceSynchronize();
+    for (int k = 0; k < kRing; k++) {
+      (void)hipFree(d_spheres[k]);
+      (void)hipHostFree(h_spheres[k]);
+      if (spheres_ev[k]) (void)hipEventDestroy(spheres_ev[k]);
+    }
     (void)hipFree(d_frame);
     (void)hipHostFree(h_stage);
     if (stream) (void)hipStreamDestroy(stream);
@@ -263,10 +276,20 @@ struct sfrt_world {
 
   int ensure_sphere_buffers(int n) {
     if (n <= d_spheres_cap) return SFRT_OK;
-    for (auto*& p : d_spheres) {
-      (void)hipFree(p);
-      p = nullptr;
-      HIP_TRY(hipMalloc(&p, sizeof(sfrt::SphereRec) * (size_t)n));
+    HIP_TRY(hipDeviceSynchronize());  // launches on any stream may read the old slots
+    for (int k = 0; k < kRing; k++) {
+      (void)hipFree(d_spheres[k]);
+      (void)hipHostFree(h_spheres[k]);
+      d_spheres[k] = nullptr;
+      h_spheres[k] = nullptr;
+      spheres_pending[k] = false;
+    }
+    d_spheres_cap = 0;
+    for (int k = 0; k < kRing; k++) {
+      HIP_TRY(hipMalloc(&d_spheres[k], sizeof(sfrt::SphereRec) * (size_t)n));
+      HIP_TRY(hipHostMalloc(&h_spheres[k], sizeof(sfrt::SphereRec) * (size_t)n,
+                            hipHostMallocDefault));
+      if (!spheres_ev[k]) HIP_TRY(hipEventCreateWithFlags(&spheres_ev[k], hipEventDisableTiming));
     }
     d_spheres_cap = n;
     return SFRT_OK;
@@ -275,18 +298,31 @@ struct sfrt_world {
   // Upload sphere records when the kernel reads them from device memory.
   int stage_spheres(sfrt::FrameRec& f, const std::vector<sfrt::SphereRec>& recs, hipStream_t s,
                     bool force) {
+    staged = -1;
     if (!force && f.n <= sfrt::kInlineSpheres) {
       f.spheres = nullptr;
       return SFRT_OK;
     }
     int rc = ensure_sphere_buffers(f.n);
     if (rc) return rc;
-    sfrt::SphereRec* dst = d_spheres[ring];
+    const int k = ring;
     ring = (ring + 1) % kRing;
-    // pageable source: the runtime stages it before returning, so recs may die after this.
-    HIP_TRY(hipMemcpyAsync(dst, recs.data(), sizeof(sfrt::SphereRec) * recs.size(),
+    if (spheres_pending[k]) HIP_TRY(hipEventSynchronize(spheres_ev[k]));
+    spheres_pending[k] = false;
+    std::memcpy(h_spheres[k], recs.data(), sizeof(sfrt::SphereRec) * recs.size());
+    HIP_TRY(hipMemcpyAsync(d_spheres[k], h_spheres[k], sizeof(sfrt::SphereRec) * recs.size(),
                            hipMemcpyHostToDevice, s));
-    f.spheres = dst;
+    f.spheres = d_spheres[k];
+    staged = k;
+    return SFRT_OK;
+  }
+
+  // After the launch that reads the staged slot has been queued on s.
+  int launched(hipStream_t s) {
+    if (staged < 0) return SFRT_OK;
+    HIP_TRY(hipEventRecord(spheres_ev[staged], s));
+    spheres_pending[staged] = true;
+    staged = -1;
     return SFRT_OK;
   }
 
@@ -514,6 +550,7 @@ int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart, int yadd
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
   if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
+  if ((rc = w->launched(w->stream))) return rc;
   HIP_TRY(hipMemcpyAsync(w->h_stage, w->d_frame, px * 4, hipMemcpyDeviceToHost, w->stream));
   rc = w->read_status(w->stream);
   if (rc) return rc;
@@ -555,7 +592,8 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   f.out_pitch = pitch_bytes / 4;
   rc = w->stage_spheres(f, recs, s, false);
   if (rc) return rc;
-  return sfrt::launch_trace(f, recs.data(), s) ? SFRT_E_HIP : SFRT_OK;
+  if (sfrt::launch_trace(f, recs.data(), s)) return SFRT_E_HIP;
+  return w->launched(s);
 }
 
 int sfrt_world_check(sfrt_world* w, void* hip_stream) {
@@ -592,6 +630,7 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
   if (hipMemcpyAsync(d_ij, ij, sizeof(int32_t) * 2 * (size_t)count, hipMemcpyHostToDevice,
                      w->stream) != hipSuccess ||
       sfrt::launch_trace_points(f, d_ij, count, d_out, w->stream) ||
+      w->launched(w->stream) != SFRT_OK ||
       hipMemcpyAsync(out, d_out, sizeof(sfrt::PixelDump) * (size_t)count, hipMemcpyDeviceToHost,
                      w->stream) != hipSuccess)
     rc = SFRT_E_HIP;
@@ -654,6 +693,7 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
   if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
+  if ((rc = w->launched(w->stream))) return rc;
   HIP_TRY(hipEventRecord(slot.rendered, w->stream));
   HIP_TRY(hipStreamWaitEvent(w->copy_stream, slot.rendered, 0));
   HIP_TRY(hipMemcpyAsync(pixels, slot.d_buf, px * 4, hipMemcpyDeviceToHost, w->copy_stream));
