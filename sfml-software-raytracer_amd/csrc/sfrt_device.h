@@ -17,6 +17,15 @@ __device__ __forceinline__ float dpp(float x) {
       __builtin_bit_cast(int, x), __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
 }
 
+// A 64-bit value made wave-uniform (SGPR pair) from lane 0's copy.  The
+// builtin returns int: each half goes through uint32_t so the low word is
+// zero-extended, not sign-extended into the high word.
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
 __device__ __forceinline__ float wave_min(float v) {
   v = fminf(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
   v = fminf(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]

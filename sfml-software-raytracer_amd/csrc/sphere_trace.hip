@@ -317,9 +317,7 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
           const int rem = f.n - w * 64;
           m = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
         } else {
-          m = s_mask[wave][w];
-          m = __builtin_amdgcn_readfirstlane((unsigned)m) |
-              ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(m >> 32)) << 32);
+          m = uniform_u64(s_mask[wave][w]);
         }
         for (; m; m &= m - 1) {
           const int k = w * 64 + __builtin_ctzll(m);

@@ -184,6 +184,30 @@ def test_many_spheres_global_path(world, floor):
     assert diff_report(got, want, 640) == ""
 
 
+@pytest.mark.parametrize("n_keep", [100, 127, 180])
+def test_records_past_n_never_marched(built, floor, n_keep):
+    """Device sphere slots keep records past n from an earlier, larger scene.
+
+    Prime every slot of the ring with 192 records, then shrink the scene to
+    its first n_keep spheres: a culling-mask word whose bit 31 is set must not
+    widen to the stale indices above n (a sign-extended readfirstlane once
+    did exactly that).  n_keep sits 4..63 past a 32-bit boundary of its word.
+    """
+    import sfrt
+    full = scenes.sort_spheres(scenes.lcg_spheres(count=191, seed=4242))
+    with sfrt.World(0) as w:
+        w.load_texture(*floor)
+        w.set_scene(scenes.Scene("prime", full).posed(0.0, 0.0), 64, 64)
+        for _ in range(12):  # more renders than ring slots
+            w.render()
+        for pose in [(0.5, -0.1), (2.0, 0.05), (4.4, 0.1)]:
+            scene = scenes.Scene("kept", full[:n_keep]).posed(*pose)
+            w.set_scene(scene, 640, 360)
+            want = oracle_for(scene, 640, 360, floor).render(host_threads())
+            for _ in range(3):
+                assert diff_report(w.render(), want, 640) == "", (n_keep, pose)
+
+
 def test_ragged_sizes(world, floor):
     """Frame sizes that are not multiples of the 8x8 wave tile."""
     scene = scenes.lcg64().posed(2.0, 0.4)

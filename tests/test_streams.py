@@ -15,6 +15,14 @@ import scenes
 import voxel_scenes as vs
 
 
+def _report(got, want, w):
+    bad = np.nonzero(np.any(got.reshape(-1, 4) != want.reshape(-1, 4), axis=1))[0]
+    if bad.size == 0:
+        return ""
+    rows = bad // w
+    return f"{bad.size} pixels differ in rows {rows.min()}..{rows.max()}"
+
+
 def _streams(n):
     import torch
     return [torch.cuda.Stream() for _ in range(n)]
@@ -42,7 +50,8 @@ def test_sphere_frames_in_flight(built, floor):
         for s in ss:
             world.check(s.cuda_stream)
     for i in range(k):
-        assert np.array_equal(bufs[i].cpu().numpy().ravel(), want[i]), f"frame {i}"
+        got = bufs[i].cpu().numpy().ravel()
+        assert np.array_equal(got, want[i]), f"frame {i}: {_report(got, want[i], w)}"
 
 
 @pytest.mark.gpu
@@ -68,7 +77,8 @@ def test_voxel_frames_in_flight(built):
         for s in ss:
             v.check(s.cuda_stream)
     for i in range(k):
-        assert np.array_equal(bufs[i].cpu().numpy().ravel(), want[i]), f"frame {i}"
+        got = bufs[i].cpu().numpy().ravel()
+        assert np.array_equal(got, want[i]), f"frame {i}: {_report(got, want[i], w)}"
 
 
 @pytest.mark.gpu
@@ -92,4 +102,5 @@ def test_glsl_frames_in_flight(built, floor):
         for st in ss:
             s.check(st.cuda_stream)
     for i in range(k):
-        assert np.array_equal(bufs[i].cpu().numpy().ravel(), want[i]), f"frame {i}"
+        got = bufs[i].cpu().numpy().ravel()
+        assert np.array_equal(got, want[i]), f"frame {i}: {_report(got, want[i], w)}"
