@@ -9,14 +9,6 @@
 
 namespace sfrt {
 
-// Wave-wide minimum through DPP row ops (no LDS): min within each 16-lane
-// row, then the four row results via readlane.  Uniform result.
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-      __builtin_bit_cast(int, x), __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
-}
-
 // A 64-bit value made wave-uniform (SGPR pair) from lane 0's copy.  The
 // builtin returns int: each half goes through uint32_t so the low word is
 // zero-extended, not sign-extended into the high word.
@@ -26,18 +18,37 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-__device__ __forceinline__ float wave_min(float v) {
-  v = fminf(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
-  v = fminf(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
-  v = fminf(v, dpp<0x141>(v));  // row_half_mirror
-  v = fminf(v, dpp<0x140>(v));  // row_mirror
-  const int b = __builtin_bit_cast(int, v);
-  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
-  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
-  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
-  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
-  return fminf(fminf(r0, r1), fminf(r2, r3));
+// Wave-wide min / max of unsigned words, all in DPP: the row reduction
+// (quad_perm, half-mirror, mirror; each step one v_min_u32_dpp), then
+// row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3, so lane
+// 63 holds the wave's result.  For binary32 values >= +0 (no NaN) the bit
+// patterns order like the values, so these also reduce non-negative floats
+// with no canonicalising VALU ops.  Call with the whole wave active (DPP
+// reads inactive lanes' stale values).
+// IDENTITY (the op's neutral value) fills lanes whose row is masked off, so
+// the compiler folds each mov_dpp into the min / max itself.
+template <int CTRL, int ROW_MASK, uint32_t IDENTITY>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)IDENTITY, (int)x, CTRL, ROW_MASK, 0xf, false);
 }
+
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_reduce_u32(uint32_t v) {
+  constexpr uint32_t I = MAX ? 0u : 0xffffffffu;
+  auto op = [](uint32_t a, uint32_t b) {
+    return MAX ? __builtin_elementwise_max(a, b) : __builtin_elementwise_min(a, b);
+  };
+  v = op(v, dpp_u32<0xB1, 0xf, I>(v));   // quad_perm [1,0,3,2]
+  v = op(v, dpp_u32<0x4E, 0xf, I>(v));   // quad_perm [2,3,0,1]
+  v = op(v, dpp_u32<0x141, 0xf, I>(v));  // row_half_mirror
+  v = op(v, dpp_u32<0x140, 0xf, I>(v));  // row_mirror
+  v = op(v, dpp_u32<0x142, 0xa, I>(v));  // row_bcast:15 -> rows 1, 3
+  v = op(v, dpp_u32<0x143, 0xc, I>(v));  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) { return wave_reduce_u32<false>(v); }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) { return wave_reduce_u32<true>(v); }
 
 // sqrtf(x) correctly rounded for x >= 2^-96 (not denormal/tiny): the raw
 // v_sqrt_f32 (within 1 ulp) corrected by the two fma residual tests that the

@@ -259,6 +259,14 @@ struct sfrt_world {
       reach = reach < e ? e : reach;
     }
     f.cull_margin = 1e-3f * reach + 1e-4f;
+    // Non-finite inputs void the drift bound and the cone: visit every sphere.
+    bool finite = std::isfinite(f.cull_margin) && std::isfinite(f.first_l) &&
+                  std::isfinite(f.h_start) && std::isfinite(f.h_inc) &&
+                  std::isfinite(f.v_start) && std::isfinite(f.v_inc);
+    for (int q = 0; q < 3; q++)
+      finite = finite && std::isfinite(f.cam[q]) && std::isfinite(f.fwd[q]) &&
+               std::isfinite(f.right[q]) && std::isfinite(f.up[q]);
+    if (!finite) f.cull = 0;
     f.tex = d_tex;
     f.status = d_status;
     recs.resize(spheres.size());

@@ -117,9 +117,10 @@ __device__ __forceinline__ Cone tile_cone(const FrameRec& f, int tile_x, int til
   const float cos_l = (dx * ax + dy * ay) + dz * az;
   Cone c;
   c.ax = ax; c.ay = ay; c.az = az;
-  c.sin_t = fminf(1.0f, -wave_min(-sin_l) + 1e-5f);
+  // sin_l >= +0 (inputs finite, sfrt_world.cpp): max over the bit patterns
+  c.sin_t = fminf(1.0f, __uint_as_float(wave_max_u32(__float_as_uint(sin_l))) + 1e-5f);
   c.cos_t = __builtin_sqrtf(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
-  c.wide = wave_min(cos_l) < 0.5f;
+  c.wide = __builtin_amdgcn_ballot_w64(cos_l < 0.5f) != 0;  // min over lanes < 0.5
   return c;
 }
 
@@ -152,6 +153,55 @@ __device__ __forceinline__ uint64_t cull_mask(const FrameRec& f, const SphereRec
       // within rr of that region: there it is still a lower bound)
       const bool side = t * c.cos_t + perp * c.sin_t >= -rr;
       inc = c.wide || wl <= rr || (side && perp * c.cos_t - t * c.sin_t <= rr);
+    }
+  }
+  return __builtin_amdgcn_ballot_w64(inc);
+}
+
+// Cull plus march window.  As cull_mask; in addition lane l returns, for
+// sphere base + l, an interval (lo, hi) of along-ray distance outside which
+// the sphere cannot pass for any ray of the cone.  A ray's march position p
+// at along-ray distance tau lies within the drift bound of the ray's point
+// cam + u*tau (cull_margin), and |cam + u*tau - c| >= |tau - dot(c - cam, u)|,
+// so a pass needs |tau - dot(w, u)| < r + drift.  Over the cone's rays
+// dot(w, u) = |w| cos(angle(w, u)) with the angle in
+// [max(0, alpha - theta), min(pi, alpha + theta)] (alpha = angle(w, axis),
+// theta = half-angle): |w| cos(alpha -+ theta) = t cos_t +- perp sin_t,
+// clamped to +-|w| where alpha - theta < 0 or alpha + theta > pi.  The
+// interval is widened by r + 2 * cull_margin: the drift, the binary32 error
+// of the lanes' accumulated distance (<= 1.3e-4 R over kCullSafeIterations
+// steps) and of these expressions all fit in the second margin.
+__device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereRec* __restrict__ sph,
+                                                int base, const Cone& c, float& lo, float& hi) {
+  const int k = base + (int)(threadIdx.x & 63);
+  bool inc = false;
+  lo = __builtin_inff();
+  hi = -__builtin_inff();
+  if (k < f.n) {
+    const SphereRec s = sph[k];
+    if (s.s_pass > 0.0f) {
+      const float wx = s.cx - f.cam[0], wy = s.cy - f.cam[1], wz = s.cz - f.cam[2];
+      const float wl = __builtin_sqrtf((wx * wx + wy * wy) + wz * wz);
+      const float rr = s.r + f.cull_margin + 4e-6f * wl;
+      const float t = (wx * c.ax + wy * c.ay) + wz * c.az;
+      const float px = wx - t * c.ax, py = wy - t * c.ay, pz = wz - t * c.az;
+      const float perp = __builtin_sqrtf((px * px + py * py) + pz * pz);
+      const bool side = t * c.cos_t + perp * c.sin_t >= -rr;
+      const float sa = perp * c.cos_t - t * c.sin_t;  // |w| sin(alpha - theta)
+      inc = c.wide || wl <= rr || (side && sa <= rr);
+      if (inc) {
+        if (c.wide) {
+          hi = __builtin_inff();
+          lo = -__builtin_inff();
+        } else {
+          const float sb = perp * c.cos_t + t * c.sin_t;  // |w| sin(alpha + theta)
+          const float up = sa >= 0.0f ? t * c.cos_t + perp * c.sin_t : wl;
+          const float dn = sb >= 0.0f ? t * c.cos_t - perp * c.sin_t : -wl;
+          const float ext = rr + f.cull_margin;
+          lo = dn - ext;
+          hi = up + ext;
+        }
+      }
     }
   }
   return __builtin_amdgcn_ballot_w64(inc);
@@ -344,6 +394,144 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
   f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
 }
 
+// n <= 64 with the march window: each step visits only the culled spheres
+// whose (lo, hi) interval meets the along-ray distances of the wave's
+// marching lanes, [min over marching lanes, max over all lanes] of tacc.
+// Lanes only move forward, so a sphere left behind by every marching lane is
+// never needed again and one not yet reached is not needed yet.
+template <int SLOTS>
+__device__ __forceinline__ void trace_tile_window(const FrameRec& f,
+                                                  const SphereRec* __restrict__ sph) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x * kWavesPerBlock + wave;
+  const int tile_y = tile / f.tiles_x;
+  const int tile_x = tile - tile_y * f.tiles_x;
+  if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
+  const int a = tile_x * kTile + (lane & 7);
+  const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
+  const int b_end = f.sub_row0 + f.sub_rows;
+  const bool valid = a < f.sub_w && b < b_end;
+  const int ac = a < f.sub_w ? a : f.sub_w - 1;
+  const int bc = b < b_end ? b : b_end - 1;
+  const int i = f.xstart + ac * f.xadd;
+  const int j = f.ystart + bc * f.yadd;
+
+  float dx, dy, dz;
+  primary_dir(f, i, j, dx, dy, dz);
+
+  const float l0 = f.first_l;
+  float px = f.cam[0] + dx * l0;
+  float py = f.cam[1] + dy * l0;
+  float pz = f.cam[2] + dz * l0;
+  int draw = f.first_draw;
+  float mv = (valid && l0 > 0.0f) ? 1.0f : 0.0f;
+  float tacc = l0;  // along-ray distance marched (binary32 sum of the steps)
+
+  const uint64_t all = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
+  const bool any_march = __builtin_amdgcn_ballot_w64(mv > 0.0f) != 0;
+  const bool windowed = f.cull && any_march;
+  uint64_t m = all;
+  float lo = -__builtin_inff(), hi = __builtin_inff();
+  if (windowed) {
+    const Cone cone = tile_cone(f, tile_x, tile_y, dx, dy, dz);
+    m = cull_window(f, sph, 0, cone, lo, hi);
+  }
+  int trips = 1;
+  if (SLOTS > 0 && windowed && __builtin_popcountll(m) <= SLOTS) {
+    // Few culled spheres: hold them in SGPR slots and test every one each
+    // step (cheaper than maintaining the window).
+    constexpr int NS = SLOTS > 0 ? SLOTS : 1;
+    float scx[NS], scy[NS], scz[NS], sr[NS], ssp[NS];
+    int sk[NS];
+    uint64_t mm = m;
+#pragma unroll
+    for (int q = 0; q < SLOTS; q++) {
+      scx[q] = scy[q] = scz[q] = sr[q] = ssp[q] = 0.0f;
+      sk[q] = 0;
+      if (mm) {
+        const int k = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        scx[q] = sph[k].cx; scy[q] = sph[k].cy; scz[q] = sph[k].cz;
+        sr[q] = sph[k].r; ssp[q] = sph[k].s_pass;
+        sk[q] = k;
+      }
+    }
+    uint64_t rest = 0;
+    while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
+      if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
+#pragma unroll
+        for (int q = 0; q < SLOTS; q++) ssp[q] = 0.0f;
+        rest = all;
+      }
+      float L = 0.0f;
+      int dnew = draw;
+      float ssq[NS];
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) ssq[q] = dist2(px, py, pz, scx[q], scy[q], scz[q]);
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) pass_body(ssq[q] < ssp[q], ssq[q], sr[q], sk[q], L, dnew);
+      for (uint64_t r2 = rest; r2; r2 &= r2 - 1) {
+        const int k = __builtin_ctzll(r2);
+        const SphereRec& s = sph[k];
+        sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      }
+      if (mv > 0.0f) {
+        px = px + dx * L;
+        py = py + dy * L;
+        pz = pz + dz * L;
+        draw = dnew;
+        mv = L;
+      }
+      if (++trips >= kMaxIterations) {
+        if (mv > 0.0f) atomicOr(f.status, 1);
+        break;
+      }
+    }
+  } else {
+    bool full = !windowed;
+    while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
+      if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
+      uint64_t win = all;
+      if (!full) {
+        // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32)
+        const float tlo = __uint_as_float(
+            wave_min_u32(__float_as_uint(mv > 0.0f ? tacc : __builtin_inff())));
+        const float thi = __uint_as_float(wave_max_u32(__float_as_uint(tacc)));
+        win = m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
+      }
+      float L = 0.0f;
+      int dnew = draw;
+      for (uint64_t mm = win; mm; mm &= mm - 1) {
+        const int k = __builtin_ctzll(mm);
+        const SphereRec& s = sph[k];
+        sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      }
+      if (mv > 0.0f) {
+        px = px + dx * L;
+        py = py + dy * L;
+        pz = pz + dz * L;
+        draw = dnew;
+        mv = L;
+        tacc = tacc + L;
+      }
+      if (++trips >= kMaxIterations) {
+        if (mv > 0.0f) atomicOr(f.status, 1);
+        break;
+      }
+    }
+  }
+  if (!valid) return;
+  const SphereRec d = sph[draw];
+  const uint32_t rgba = shade(f, d, px, py, pz, nullptr);
+  f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
+}
+
+template <int SLOTS>
+__global__ __launch_bounds__(256) void k_trace_window(InlineArgs args) {
+  trace_tile_window<SLOTS>(args.f, args.s);
+}
+
 template <int SLOTS, bool REST_LDS>
 __global__ __launch_bounds__(256) void k_trace_inline(InlineArgs args) {
   if (REST_LDS) {  // spheres beyond the slots read from an LDS copy instead of s_load
@@ -354,6 +542,105 @@ __global__ __launch_bounds__(256) void k_trace_inline(InlineArgs args) {
   } else {
     trace_tile<true, SLOTS>(args.f, args.s, args.s);
   }
+}
+
+// n > 64 with the march window: per culling word, the lanes' (lo, hi) pairs
+// live in dynamic LDS ([wave][lo/hi][n rounded up to 64] floats).
+__device__ __forceinline__ void trace_tile_window_global(const FrameRec& f,
+                                                         const SphereRec* __restrict__ sph,
+                                                         float* __restrict__ s_win) {
+  __shared__ uint64_t s_mask[kWavesPerBlock][kMaskWords];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x * kWavesPerBlock + wave;
+  const int tile_y = tile / f.tiles_x;
+  const int tile_x = tile - tile_y * f.tiles_x;
+  if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
+  const int a = tile_x * kTile + (lane & 7);
+  const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
+  const int b_end = f.sub_row0 + f.sub_rows;
+  const bool valid = a < f.sub_w && b < b_end;
+  const int ac = a < f.sub_w ? a : f.sub_w - 1;
+  const int bc = b < b_end ? b : b_end - 1;
+  const int i = f.xstart + ac * f.xadd;
+  const int j = f.ystart + bc * f.yadd;
+
+  float dx, dy, dz;
+  primary_dir(f, i, j, dx, dy, dz);
+
+  const float l0 = f.first_l;
+  float px = f.cam[0] + dx * l0;
+  float py = f.cam[1] + dy * l0;
+  float pz = f.cam[2] + dz * l0;
+  int draw = f.first_draw;
+  float mv = (valid && l0 > 0.0f) ? 1.0f : 0.0f;
+  float tacc = l0;
+
+  const int nwords = (f.n + 63) >> 6;
+  float* const w_lo = s_win + (size_t)wave * 2 * nwords * 64;
+  float* const w_hi = w_lo + nwords * 64;
+  const bool any_march = __builtin_amdgcn_ballot_w64(mv > 0.0f) != 0;
+  const bool windowed = f.cull && any_march;
+  if (windowed) {
+    const Cone cone = tile_cone(f, tile_x, tile_y, dx, dy, dz);
+    for (int w = 0; w < nwords; w++) {
+      float lo, hi;
+      const uint64_t m = cull_window(f, sph, w * 64, cone, lo, hi);
+      if (lane == 0) s_mask[wave][w] = m;
+      w_lo[w * 64 + lane] = lo;
+      w_hi[w * 64 + lane] = hi;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  int trips = 1;
+  bool full = !windowed;
+  while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
+    if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
+    float tlo = 0.0f, thi = 0.0f;
+    if (!full) {
+      tlo = __uint_as_float(wave_min_u32(__float_as_uint(mv > 0.0f ? tacc : __builtin_inff())));
+      thi = __uint_as_float(wave_max_u32(__float_as_uint(tacc)));
+    }
+    float L = 0.0f;
+    int dnew = draw;
+    for (int w = 0; w < nwords; w++) {
+      uint64_t win;
+      if (full) {
+        const int rem = f.n - w * 64;
+        win = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
+      } else {
+        win = uniform_u64(s_mask[wave][w]) &
+              __builtin_amdgcn_ballot_w64(w_lo[w * 64 + lane] < thi) &
+              __builtin_amdgcn_ballot_w64(w_hi[w * 64 + lane] > tlo);
+      }
+      for (; win; win &= win - 1) {
+        const int k = w * 64 + __builtin_ctzll(win);
+        const SphereRec& s = sph[k];
+        sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      }
+    }
+    if (mv > 0.0f) {
+      px = px + dx * L;
+      py = py + dy * L;
+      pz = pz + dz * L;
+      draw = dnew;
+      mv = L;
+      tacc = tacc + L;
+    }
+    if (++trips >= kMaxIterations) {
+      if (mv > 0.0f) atomicOr(f.status, 1);
+      break;
+    }
+  }
+  if (!valid) return;
+  const SphereRec d = sph[draw];
+  const uint32_t rgba = shade(f, d, px, py, pz, nullptr);
+  f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
+}
+
+__global__ __launch_bounds__(256) void k_trace_global_window(FrameRec f) {
+  extern __shared__ float s_win[];
+  trace_tile_window_global(f, f.spheres, s_win);
 }
 
 __global__ __launch_bounds__(256) void k_trace_global(FrameRec f) {
@@ -412,7 +699,10 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     InlineArgs args;
     args.f = f;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    // SFRT_OPT_VARIANT (tuning A/B only): number of SGPR sphere slots; 0 = kSlots.
+    // SFRT_OPT_VARIANT (tuning A/B only).  Default: march window with the
+    // SGPR-slot march for waves with <= kSlots culled spheres; 2: slots + the
+    // rest every step (no window); 1/6/8: slot counts; 16/17: LDS-backed
+    // rest; 32/36: window with 0/6 slots.
     const dim3 g((unsigned)blocks), b(256);
     switch (f.variant) {
       case 1: hipLaunchKernelGGL((k_trace_inline<0, false>), g, b, 0, s, args); break;
@@ -420,10 +710,18 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
       case 8: hipLaunchKernelGGL((k_trace_inline<8, false>), g, b, 0, s, args); break;
       case 16: hipLaunchKernelGGL((k_trace_inline<kSlots, true>), g, b, 0, s, args); break;
       case 17: hipLaunchKernelGGL((k_trace_inline<0, true>), g, b, 0, s, args); break;
-      default: hipLaunchKernelGGL((k_trace_inline<kSlots, false>), g, b, 0, s, args); break;
+      case 2: hipLaunchKernelGGL((k_trace_inline<kSlots, false>), g, b, 0, s, args); break;
+      case 32: hipLaunchKernelGGL(k_trace_window<0>, g, b, 0, s, args); break;
+      case 36: hipLaunchKernelGGL(k_trace_window<6>, g, b, 0, s, args); break;
+      default: hipLaunchKernelGGL(k_trace_window<kSlots>, g, b, 0, s, args); break;
     }
   } else {
-    hipLaunchKernelGGL(k_trace_global, dim3((unsigned)blocks), dim3(256), 0, s, f);
+    if (f.variant == 2) {  // A/B: the per-word culled lists visited every step
+      hipLaunchKernelGGL(k_trace_global, dim3((unsigned)blocks), dim3(256), 0, s, f);
+    } else {
+      const size_t lds = (size_t)kWavesPerBlock * 2 * (size_t)((f.n + 63) / 64) * 64 * sizeof(float);
+      hipLaunchKernelGGL(k_trace_global_window, dim3((unsigned)blocks), dim3(256), lds, s, f);
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

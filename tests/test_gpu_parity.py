@@ -95,19 +95,48 @@ def test_cull_on_off_identical(world, floor):
     assert diff_report(a, b, 3840) == ""
 
 
-@pytest.mark.parametrize("variant", [1, 6, 8, 16, 17])
+@pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 36])
 def test_kernel_variants_identical(world, floor, variant):
     """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
     produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
     import sfrt
-    world.set_scene(scenes.lcg64().posed(1.1, -0.2), 3840, 2160)
-    a = world.render()
-    world.set_option(sfrt.SFRT_OPT_VARIANT, variant)
-    try:
-        b = world.render()
-    finally:
-        world.set_option(sfrt.SFRT_OPT_VARIANT, 0)
-    assert diff_report(a, b, 3840) == ""
+    cases = [(scenes.lcg64(), (1.1, -0.2), 3840, 2160)]
+    rng = np.random.default_rng(variant)
+    for sc in (scenes.lcg64(), scenes.default10(), scenes.one_sphere()):
+        for _ in range(4):
+            cases.append((sc, (float(rng.uniform(0, 6.3)), float(rng.uniform(-0.6, 0.6))), 1000, 563))
+    for sc, pose, width, height in cases:
+        world.set_scene(sc.posed(*pose), width, height)
+        a = world.render()
+        world.set_option(sfrt.SFRT_OPT_VARIANT, variant)
+        try:
+            b = world.render()
+        finally:
+            world.set_option(sfrt.SFRT_OPT_VARIANT, 0)
+        assert diff_report(a, b, width) == "", (sc.name, pose)
+
+
+@pytest.mark.parametrize("count", [65, 120, 199, 1023])
+def test_global_window_matches_word_lists(world, floor, count):
+    """n > 64: the windowed kernel equals the per-word culled-list kernel
+    (variant 2) for several poses, and the oracle for one of them."""
+    import sfrt
+    spheres = scenes.sort_spheres(scenes.lcg_spheres(count=count - 1, seed=31 + count))
+    rng = np.random.default_rng(count)
+    for q in range(4):
+        pose = (float(rng.uniform(0, 6.3)), float(rng.uniform(-0.6, 0.6)))
+        scene = scenes.Scene("many", spheres).posed(*pose)
+        world.set_scene(scene, 1000, 563)
+        a = world.render()
+        world.set_option(sfrt.SFRT_OPT_VARIANT, 2)
+        try:
+            b = world.render()
+        finally:
+            world.set_option(sfrt.SFRT_OPT_VARIANT, 0)
+        assert diff_report(a, b, 1000) == "", (count, pose)
+        if q == 0 and count <= 200:
+            want = oracle_for(scene, 1000, 563, floor).render(host_threads())
+            assert diff_report(a, want, 1000) == "", (count, pose)
 
 
 @pytest.mark.parametrize("ystart,yadd,xstart,xadd", [
@@ -252,6 +281,16 @@ def test_device_div_recip(tmp_path):
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                     "-ffp-contract=off", src, "-o", str(exe)], check=True, capture_output=True)
     r = subprocess.run([str(exe), "33"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
+
+
+def test_wave_helpers(tmp_path):
+    """wave_min_u32 / wave_max_u32 / uniform_u64 (sfrt_device.h) against a lane loop."""
+    exe = tmp_path / "wave_check"
+    src = os.path.join(ROOT, "tests", "native", "wave_check.hip")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    src, "-o", str(exe)], check=True, capture_output=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
 
 
