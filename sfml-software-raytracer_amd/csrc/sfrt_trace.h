@@ -23,6 +23,7 @@ constexpr int kMaxIterations = 1 << 20;  // march guard; the reference has none
 // positions stays below the culling margin, see cull_margin); a wave that
 // goes further switches to the full sphere list for the rest of its march.
 constexpr int kCullSafeIterations = 1024;
+constexpr int kPairMinSpheres = 16;  // above this, n <= 64 frames use 16x8 tiles (2 px per lane)
 constexpr int kSlots = 4;             // culled spheres held in SGPRs per wave (measured best of 0,4,6,8)
 
 // One sphere as the kernel reads it: 32 B, one s_load_dwordx8.

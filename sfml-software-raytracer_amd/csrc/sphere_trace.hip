@@ -527,6 +527,236 @@ __device__ __forceinline__ void trace_tile_window(const FrameRec& f,
   f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
 }
 
+// R pixels per lane (an (8R)x8 tile per wave: columns c, c + 8, ...): the
+// wave-uniform work of a sphere visit -- record load, window bits, branch --
+// is shared by R rays, and each lane carries R independent dependency chains.
+// Same exact march as trace_tile_window, per ray.
+template <int R>
+__device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int tile_y,
+                                            const float (&dx)[R], const float (&dy)[R],
+                                            const float (&dz)[R]) {
+  const float ic = (float)f.xstart +
+                   ((float)(tile_x * R * kTile) + (0.5f * (float)(R * kTile) - 0.5f)) * (float)f.xadd;
+  const float jc = (float)f.ystart +
+                   ((float)(f.sub_row0 + tile_y * kTile) + 3.5f) * (float)f.yadd;
+  const float h = f.h_start + f.h_inc * ic;
+  const float v = f.v_start + jc * f.v_inc;
+  float ax = (f.fwd[0] + f.right[0] * h) + f.up[0] * v;
+  float ay = (f.fwd[1] + f.right[1] * h) + f.up[1] * v;
+  float az = (f.fwd[2] + f.right[2] * h) + f.up[2] * v;
+  const float inv = __builtin_amdgcn_rsqf((ax * ax + ay * ay) + az * az);
+  ax *= inv; ay *= inv; az *= inv;
+  float sin_l = 0.0f;
+  bool wide = false;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const float cx = dy[r] * az - dz[r] * ay, cy = dz[r] * ax - dx[r] * az,
+                cz = dx[r] * ay - dy[r] * ax;
+    sin_l = fmaxf(sin_l, __builtin_sqrtf((cx * cx + cy * cy) + cz * cz));
+    wide = wide || ((dx[r] * ax + dy[r] * ay) + dz[r] * az) < 0.5f;
+  }
+  Cone c;
+  c.ax = ax; c.ay = ay; c.az = az;
+  c.sin_t = fminf(1.0f, __uint_as_float(wave_max_u32(__float_as_uint(sin_l))) + 1e-5f);
+  c.cos_t = __builtin_sqrtf(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
+  c.wide = __builtin_amdgcn_ballot_w64(wide) != 0;
+  return c;
+}
+
+// Pass bodies of one sphere for the lane's R rays under one scalar branch.
+template <int R>
+__device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, float rad, int k,
+                                            float (&L)[R], int (&dnew)[R]) {
+  uint64_t pm[R], any = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    pm[r] = __builtin_amdgcn_ballot_w64(ss[r] < s_pass);
+    any |= pm[r];
+  }
+  if (any) {
+    __asm__ volatile("; sphere passes for some ray of the wave");
+    uint64_t tiny = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) tiny |= __builtin_amdgcn_ballot_w64(ss[r] < kTinySqrtArg) & pm[r];
+    if (tiny == 0) {
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (ss[r] < s_pass) {
+          const float t = rad - sqrt_cr_normal(ss[r]);
+          L[r] = L[r] < t ? t : L[r];
+          dnew[r] = k;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (ss[r] < s_pass) {
+          const float t = rad - __builtin_sqrtf(ss[r]);
+          L[r] = L[r] < t ? t : L[r];
+          dnew[r] = k;
+        }
+      }
+    }
+  }
+}
+
+template <int SLOTS, int R>
+__device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
+                                                    const SphereRec* __restrict__ sph) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile = blockIdx.x * kWavesPerBlock + wave;
+  const int tile_y = tile / f.tiles_x;  // f.tiles_x = ceil(sub_w / (8 R)) for this kernel
+  const int tile_x = tile - tile_y * f.tiles_x;
+  if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
+  const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
+  const int b_end = f.sub_row0 + f.sub_rows;
+  const int bc = b < b_end ? b : b_end - 1;
+  const int j = f.ystart + bc * f.yadd;
+  const float l0 = f.first_l;
+  int a[R], draw[R];
+  bool valid[R];
+  float dx[R], dy[R], dz[R], px[R], py[R], pz[R], mv[R], tacc[R];
+  bool marching = false;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    a[r] = tile_x * R * kTile + r * kTile + (lane & 7);
+    valid[r] = a[r] < f.sub_w && b < b_end;
+    const int ac = a[r] < f.sub_w ? a[r] : f.sub_w - 1;
+    primary_dir(f, f.xstart + ac * f.xadd, j, dx[r], dy[r], dz[r]);
+    px[r] = f.cam[0] + dx[r] * l0;
+    py[r] = f.cam[1] + dy[r] * l0;
+    pz[r] = f.cam[2] + dz[r] * l0;
+    draw[r] = f.first_draw;
+    mv[r] = (valid[r] && l0 > 0.0f) ? 1.0f : 0.0f;
+    tacc[r] = l0;
+    marching = marching || mv[r] > 0.0f;
+  }
+  auto any_marching = [&]() {
+    bool q = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) q = q || mv[r] > 0.0f;
+    return __builtin_amdgcn_ballot_w64(q) != 0;
+  };
+  const uint64_t all = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
+  const bool windowed = f.cull && __builtin_amdgcn_ballot_w64(marching) != 0;
+  uint64_t m = all;
+  float lo = -__builtin_inff(), hi = __builtin_inff();
+  if (windowed) {
+    const Cone cone = tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
+    m = cull_window(f, sph, 0, cone, lo, hi);
+  }
+  auto advance = [&](const float (&L)[R], const int (&dnew)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (mv[r] > 0.0f) {
+        px[r] = px[r] + dx[r] * L[r];
+        py[r] = py[r] + dy[r] * L[r];
+        pz[r] = pz[r] + dz[r] * L[r];
+        draw[r] = dnew[r];
+        mv[r] = L[r];
+        tacc[r] = tacc[r] + L[r];
+      }
+    }
+  };
+  auto visit = [&](float cx, float cy, float cz, float rad, float s_pass, int k, float (&L)[R],
+                   int (&dnew)[R]) {
+    float ss[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) ss[r] = dist2(px[r], py[r], pz[r], cx, cy, cz);
+    pass_body_r<R>(ss, s_pass, rad, k, L, dnew);
+  };
+  int trips = 1;
+  if (SLOTS > 0 && windowed && __builtin_popcountll(m) <= SLOTS) {
+    constexpr int NS = SLOTS > 0 ? SLOTS : 1;
+    float scx[NS], scy[NS], scz[NS], sr[NS], ssp[NS];
+    int sk[NS];
+    uint64_t mm = m;
+#pragma unroll
+    for (int q = 0; q < SLOTS; q++) {
+      scx[q] = scy[q] = scz[q] = sr[q] = ssp[q] = 0.0f;
+      sk[q] = 0;
+      if (mm) {
+        const int k = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        scx[q] = sph[k].cx; scy[q] = sph[k].cy; scz[q] = sph[k].cz;
+        sr[q] = sph[k].r; ssp[q] = sph[k].s_pass;
+        sk[q] = k;
+      }
+    }
+    uint64_t rest = 0;
+    while (any_marching()) {
+      if (trips == kCullSafeIterations) {
+#pragma unroll
+        for (int q = 0; q < SLOTS; q++) ssp[q] = 0.0f;
+        rest = all;
+      }
+      float L[R];
+      int dnew[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
+#pragma unroll
+      for (int q = 0; q < SLOTS; q++) visit(scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L, dnew);
+      for (uint64_t r2 = rest; r2; r2 &= r2 - 1) {
+        const int k = __builtin_ctzll(r2);
+        const SphereRec& s = sph[k];
+        visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      }
+      advance(L, dnew);
+      if (++trips >= kMaxIterations) {
+        if (any_marching() && lane == 0) atomicOr(f.status, 1);
+        break;
+      }
+    }
+  } else {
+    bool full = !windowed;
+    while (any_marching()) {
+      if (trips == kCullSafeIterations) full = true;
+      uint64_t win = all;
+      if (!full) {
+        uint32_t tl = 0x7f800000u, th = 0u;  // +inf, +0
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const uint32_t u = __float_as_uint(tacc[r]);
+          const uint32_t ua = mv[r] > 0.0f ? u : 0x7f800000u;
+          tl = ua < tl ? ua : tl;
+          th = u > th ? u : th;
+        }
+        const float tlo = __uint_as_float(wave_min_u32(tl));
+        const float thi = __uint_as_float(wave_max_u32(th));
+        win = m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
+      }
+      float L[R];
+      int dnew[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
+      for (uint64_t mm = win; mm; mm &= mm - 1) {
+        const int k = __builtin_ctzll(mm);
+        const SphereRec& s = sph[k];
+        visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      }
+      advance(L, dnew);
+      if (++trips >= kMaxIterations) {
+        if (any_marching() && lane == 0) atomicOr(f.status, 1);
+        break;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (valid[r]) {
+      const SphereRec d = sph[draw[r]];
+      const uint32_t rgba = shade(f, d, px[r], py[r], pz[r], nullptr);
+      f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] = rgba;
+    }
+  }
+}
+
+template <int SLOTS, int R>
+__global__ __launch_bounds__(256) void k_trace_window_r(InlineArgs args) {
+  trace_tile_window_r<SLOTS, R>(args.f, args.s);
+}
+
 template <int SLOTS>
 __global__ __launch_bounds__(256) void k_trace_window(InlineArgs args) {
   trace_tile_window<SLOTS>(args.f, args.s);
@@ -695,14 +925,38 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
   const long long blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > 0x7fffffffLL) return -1;
   hipStream_t s = (hipStream_t)stream;
-  if (f.n <= kInlineSpheres) {
+  // Default for n <= 64: 16x8 tiles (two pixels per lane) once the scene has
+  // more than kPairMinSpheres spheres; with few spheres the 8x8 kernel's
+  // tighter tiles win (measured).
+  const int rays = f.variant == 40 || f.variant == 41 ? 2
+                   : f.variant == 42 ? 3
+                   : f.variant == 43 ? 4
+                   : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
+  if (f.n <= kInlineSpheres && rays > 1) {
+    // (8 rays) x 8 tiles: several pixels per lane
+    InlineArgs args;
+    args.f = f;
+    args.f.tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
+    for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
+    const dim3 g2((unsigned)((tiles_y * args.f.tiles_x + kWavesPerBlock - 1) / kWavesPerBlock));
+    if (f.variant == 41)
+      hipLaunchKernelGGL((k_trace_window_r<0, 2>), g2, dim3(256), 0, s, args);
+    else if (rays == 3)
+      hipLaunchKernelGGL((k_trace_window_r<kSlots, 3>), g2, dim3(256), 0, s, args);
+    else if (rays == 4)
+      hipLaunchKernelGGL((k_trace_window_r<kSlots, 4>), g2, dim3(256), 0, s, args);
+    else
+      hipLaunchKernelGGL((k_trace_window_r<kSlots, 2>), g2, dim3(256), 0, s, args);
+  } else if (f.n <= kInlineSpheres) {
     InlineArgs args;
     args.f = f;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    // SFRT_OPT_VARIANT (tuning A/B only).  Default: march window with the
-    // SGPR-slot march for waves with <= kSlots culled spheres; 2: slots + the
-    // rest every step (no window); 1/6/8: slot counts; 16/17: LDS-backed
-    // rest; 32/36: window with 0/6 slots.
+    // SFRT_OPT_VARIANT (tuning A/B only).  Default (8x8 tiles): march window
+    // with the SGPR-slot march for waves with <= kSlots culled spheres; 35:
+    // that kernel whatever n; 40/41: the 16x8 pair kernel with 4/0 slots;
+    // 42/43: 24x8 / 32x8 tiles (3 / 4 pixels per lane);
+    // 2: slots + the rest every step (no window); 1/6/8: slot counts; 16/17:
+    // LDS-backed rest; 32/36: window with 0/6 slots.
     const dim3 g((unsigned)blocks), b(256);
     switch (f.variant) {
       case 1: hipLaunchKernelGGL((k_trace_inline<0, false>), g, b, 0, s, args); break;
@@ -713,6 +967,7 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
       case 2: hipLaunchKernelGGL((k_trace_inline<kSlots, false>), g, b, 0, s, args); break;
       case 32: hipLaunchKernelGGL(k_trace_window<0>, g, b, 0, s, args); break;
       case 36: hipLaunchKernelGGL(k_trace_window<6>, g, b, 0, s, args); break;
+      case 35:
       default: hipLaunchKernelGGL(k_trace_window<kSlots>, g, b, 0, s, args); break;
     }
   } else {

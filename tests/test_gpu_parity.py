@@ -95,7 +95,7 @@ def test_cull_on_off_identical(world, floor):
     assert diff_report(a, b, 3840) == ""
 
 
-@pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 36])
+@pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 35, 36, 40, 41, 42, 43])
 def test_kernel_variants_identical(world, floor, variant):
     """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
     produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
