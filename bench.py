@@ -46,7 +46,7 @@ BYTES_PER_RAY = 4            # RGBA8 store; texture + sphere table are cache-res
 WIDTH, ROWS_PER_GPU = 3840, 2160
 
 
-def measured_traffic(grid_threads: int):
+def measured_traffic(pixels: int):
     """Per-launch HBM bytes and VALU instruction counts of this workload from the
     newest profiles/*_traffic.json (tools/rocprof_summary.py over separate
     rocprofv3 --pmc passes of this same command), or None."""
@@ -55,7 +55,7 @@ def measured_traffic(grid_threads: int):
         doc = json.load(open(path))
         if doc.get("kernel", "k_trace") != "k_trace":
             continue
-        ent = doc["per_grid_threads"].get(str(grid_threads))
+        ent = doc.get("per_launch_pixels", doc.get("per_grid_threads", {})).get(str(pixels))
         if ent:
             return ent, os.path.relpath(path, ROOT)
     return None, None

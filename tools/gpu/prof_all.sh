@@ -13,7 +13,9 @@ run() {  # name, then the command after --
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/${name}_write -o run --output-format csv -- "$@" > $O/${name}_write.log 2>&1 || return 1
   timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/${name}_sq -o run --output-format csv -- "$@" > $O/${name}_sq.log 2>&1 || return 1
 }
-run sphere python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit 1
-run glsl python3 tools/bench_glsl.py --no-cpu --steps 10 || exit 1
-run voxel python3 tools/bench_voxel.py --no-cpu --steps 10 || exit 1
+# ONLY=sphere|glsl|voxel limits the passes to one renderer
+want() { [ -z "$ONLY" ] || [ "$ONLY" = "$1" ]; }
+if want sphere; then run sphere python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline || exit 1; fi
+if want glsl; then run glsl python3 tools/bench_glsl.py --no-cpu --steps 10 || exit 1; fi
+if want voxel; then run voxel python3 tools/bench_voxel.py --no-cpu --steps 10 || exit 1; fi
 echo ALLDONE

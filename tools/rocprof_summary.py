@@ -6,6 +6,8 @@
 Writes
   profiles/<tag>_kernel_stats_by_grid.csv  per (kernel, grid size): calls, avg/min/max ns
   profiles/<tag>_traffic.json              HBM bytes per launch of the trace kernels,
+                                           keyed by pixels per launch (grid threads x
+                                           pixels per thread),
                                            from separate --pmc FETCH_SIZE / WRITE_SIZE passes,
                                            and SQ_INSTS_VALU / SQ_WAVES per launch (--sq)
 HBM bytes follow MI355X_MICROARCH.md "HBM": counters are in KiB; on gfx950
@@ -20,6 +22,13 @@ import csv
 import glob
 import json
 import os
+import re
+
+
+def pixels_per_thread(kernel_name: str) -> int:
+    """Pixels one work-item writes: R for k_trace_window_r<SLOTS, R>, else 1."""
+    m = re.search(r"k_trace_window_r<\s*\d+\s*,\s*(\d+)\s*>", kernel_name)
+    return int(m.group(1)) if m else 1
 
 
 def rows(d, name):
@@ -54,14 +63,16 @@ def main():
         acc = collections.defaultdict(list)
         for r in rows(d, "counter_collection"):
             if a.kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                acc[int(r["Grid_Size"])].append(float(r["Counter_Value"]) * 1024.0)
+                px = int(r["Grid_Size"]) * pixels_per_thread(r["Kernel_Name"])
+                acc[px].append(float(r["Counter_Value"]) * 1024.0)
         for grid, v in acc.items():
             traffic.setdefault(str(grid), {})[counter] = sum(v) / len(v)
     if a.sq:
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in rows(a.sq, "counter_collection"):
             if a.kernel in r["Kernel_Name"]:
-                acc[int(r["Grid_Size"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                px = int(r["Grid_Size"]) * pixels_per_thread(r["Kernel_Name"])
+                acc[px][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for grid, cs in acc.items():
             for c, v in cs.items():
                 traffic.setdefault(str(grid), {})[c] = sum(v) / len(v)
@@ -70,7 +81,7 @@ def main():
         t["algorithmic_bytes_per_launch"] = 4.0 * int(g)
     with open(os.path.join(a.out, f"{a.tag}_traffic.json"), "w") as f:
         json.dump({"note": __doc__.split("Writes")[0].strip(), "kernel": a.kernel,
-                   "per_grid_threads": traffic}, f, indent=1)
+                   "per_launch_pixels": traffic}, f, indent=1)
     print(json.dumps(traffic, indent=1))
 
 
