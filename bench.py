@@ -5,11 +5,16 @@
 
 A step is one full frame: every rank fills its row band of a 3840 x (2160*N)
 RGBA8 frame in HBM through libsfrt.so (64-sphere cave, BASELINE config 3),
-then for N > 1 the bands are gathered to rank 0 over RCCL, the gather of
-frame k overlapping the render of frame k+1 (double-buffered bands/frames).  Per-GPU work is
-fixed as N grows ("weak" scaling); rays use the global row index, so the
+then for N > 1 the bands travel to rank 0 over RCCL (one gather for equal
+bands, grouped point-to-point transfers otherwise), the transfer of frame k
+overlapping the render of frame k+1 (double-buffered bands/frames).  The
+band heights are tuned during the untimed warm-up (bands.tune_spans: rank 0,
+whose band never crosses a link, may take more rows).  Per-GPU work is fixed
+on average as N grows ("weak" scaling); rays use the global row index, so the
 gathered frame is byte-identical to a single-GPU render of the same frame.
 value = all rays of the K frames / (max over ranks of the timed wall time).
+Before the W warm-up frames, --settle seconds of untimed frames let the chip
+reach its steady clock (it ramps over the first few hundred frames).
 
 Also reported under "also": the 7680x4320 frame row-tiled over the N ranks
 (BASELINE config 4; N = 1, 2, 4, 8) and the 16384x16384 frame on 8 ranks
@@ -36,6 +41,8 @@ import torch.distributed as dist  # noqa: E402
 
 import scenes  # noqa: E402
 import sfrt  # noqa: E402
+from bands import (BandPipeline, band_of, max_over_ranks as _max_over_ranks,  # noqa: E402,F401
+                   tune_spans)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMD32 x one wave64 instruction per 2 clocks at
@@ -59,77 +66,6 @@ def measured_traffic(pixels: int):
         if ent:
             return ent, os.path.relpath(path, ROOT)
     return None, None
-
-
-def band_of(rank: int, world: int, height: int) -> tuple[int, int]:
-    r0 = rank * height // world
-    return r0, (rank + 1) * height // world - r0
-
-
-class BandPipeline:
-    """Row-band frames with the gather to rank 0 overlapped with rendering.
-
-    Every rank owns `depth` band buffers; rank 0 also owns `depth` whole
-    frames.  Frame k renders into band k % depth and its gather into frame
-    k % depth is queued asynchronously (RCCL runs it on its own stream after
-    the render that produced the band), so frame k+1 renders while frame k
-    crosses xGMI.  Reusing a buffer first waits (stream-side on RCCL) for the
-    gather that last read it.  Equal bands use one gather collective; unequal
-    bands one batch of point-to-point transfers into the frame's row slices.
-    With one rank the band IS the frame and nothing is exchanged."""
-
-    def __init__(self, rank: int, world_size: int, height: int, pitch: int, device, depth: int = 2):
-        self.rank, self.world_size, self.height = rank, world_size, height
-        self.depth = depth if world_size > 1 else 1
-        self.row0, self.rows = band_of(rank, world_size, height)
-        self.frames, self.views = [], []
-        if world_size == 1:
-            self.frames = [torch.empty(height, pitch, dtype=torch.uint8, device=device)]
-            self.bands = self.frames
-        else:
-            self.bands = [torch.empty(self.rows, pitch, dtype=torch.uint8, device=device)
-                          for _ in range(self.depth)]
-            if rank == 0:
-                for _ in range(self.depth):
-                    fr = torch.empty(height, pitch, dtype=torch.uint8, device=device)
-                    self.frames.append(fr)
-                    self.views.append([fr[r0:r0 + n] for r0, n in
-                                       (band_of(r, world_size, height) for r in range(world_size))])
-        self.pending = [[] for _ in range(self.depth)]
-
-    def acquire(self, k: int):
-        """The band buffer for frame k, once the gather that last read it is done."""
-        b = k % self.depth
-        for work in self.pending[b]:
-            work.wait()
-        self.pending[b] = []
-        return self.bands[b]
-
-    def submit(self, k: int) -> None:
-        """Queue frame k's gather (after everything already queued on the current stream)."""
-        if self.world_size == 1:
-            return
-        b = k % self.depth
-        band = self.bands[b]
-        views = self.views[b] if self.rank == 0 else None
-        if self.height % self.world_size == 0:
-            self.pending[b] = [dist.gather(band, views, dst=0, async_op=True)]
-        elif self.rank == 0:
-            ops = [dist.P2POp(dist.irecv, views[r], r) for r in range(1, self.world_size)]
-            views[0].copy_(band)
-            self.pending[b] = dist.batch_isend_irecv(ops)
-        else:
-            self.pending[b] = dist.batch_isend_irecv([dist.P2POp(dist.isend, band, 0)])
-
-    def drain(self) -> None:
-        for b in range(self.depth):
-            for work in self.pending[b]:
-                work.wait()
-            self.pending[b] = []
-
-    def frame(self, k: int):
-        """Rank 0's assembled frame k (valid after drain() or the next acquire of its slot)."""
-        return self.frames[k % self.depth] if self.frames else None
 
 
 def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream):
@@ -164,23 +100,50 @@ def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream):
 
 
 def max_over_ranks(x: float) -> float:
-    if not dist.is_initialized():
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _max_over_ranks(x, "cuda")
+
+
+def settle(world, pitch, row0, rows, stream, seconds: float) -> None:
+    """Untimed frames until `seconds` have passed: the chip ramps its clock over the
+    first few hundred frames after idling, and the timed frames should
+    see the steady state a continuously rendering display or offline job runs at."""
+    buf = torch.empty(rows, pitch, dtype=torch.uint8, device="cuda")
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(16):
+            world.render_band(buf.data_ptr(), pitch, row0, rows, stream.cuda_stream)
+        torch.cuda.synchronize()
+    del buf
+
+
+def tuned_pipeline(world, rank, world_size, height, pitch, stream):
+    """Row bands for this node: tune_spans times a few root-weighted partitions with
+    real frames (untimed warm-up) and keeps the fastest; N = 1 is one whole band."""
+    def render(band, row0, rows):
+        world.render_band(band.data_ptr(), pitch, row0, rows, stream.cuda_stream)
+    spans, factor, table = tune_spans(render, rank, world_size, height, pitch, "cuda",
+                                      sync=torch.cuda.synchronize, reduce_device="cuda")
+    pipe = BandPipeline(rank, world_size, height, pitch, "cuda", spans=spans)
+    info = {"rows_per_rank": [n for _, n in spans], "root_factor": factor}
+    if table:
+        info["tuning_ms_per_frame"] = {str(k): v for k, v in table.items()}
+    return pipe, info
 
 
 def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, stream):
-    """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped gather)."""
+    """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped transfer)."""
     world.set_scene(scene, width, height)
-    pipe = BandPipeline(rank, world_size, height, width * 4, "cuda")
+    pipe, bands = tuned_pipeline(world, rank, world_size, height, width * 4, stream)
     wall, kms = time_frames(world, pipe, width * 4, steps, warmup, stream)
     wall = max_over_ranks(wall)
+    rays0 = width * pipe.rows
     del pipe
     return {"n_gpus": world_size, "Mrays_per_s": round(width * height * steps / wall / 1e6, 2),
             "fps": round(steps / wall, 2), "ms_per_frame": round(wall / steps * 1e3, 4),
-            "kernel_ms_rank0_band": round(kms, 4)}
+            "kernel_ms_rank0_band": round(kms, 4),
+            "hbm_frac_rank0_kernel": round(BYTES_PER_RAY * rays0 / (kms * 1e-3) / 1e9
+                                           / HBM_PEAK_GBS, 6),
+            "bands": bands}
 
 
 # BASELINE.json configs 4 and 5 (and the 8K frame on one GPU): frame size by GPU count.
@@ -218,8 +181,10 @@ def cpu_baseline(scene, width, height, floor, gpu_frame):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--settle", type=float, default=0.3,
+                    help="seconds of untimed frames before the warm-up (clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the 8K / 16K frames")
     args = ap.parse_args()
@@ -238,7 +203,6 @@ def main() -> None:
     floor = scenes.load_floor()
     scene = scenes.lcg64()
     height = ROWS_PER_GPU * world_size
-    row0, rows = band_of(rank, world_size, height)
     pitch = WIDTH * 4
     # A dedicated stream: the kernels, the HIP events that time them and the
     # RCCL gather (which orders itself after the current stream) all use it.
@@ -248,7 +212,9 @@ def main() -> None:
     w.load_texture(*floor)
     w.set_scene(scene, WIDTH, height)
 
-    pipe = BandPipeline(rank, world_size, height, pitch, "cuda")
+    settle(w, pitch, *band_of(rank, world_size, height), stream, args.settle)
+    pipe, bands = tuned_pipeline(w, rank, world_size, height, pitch, stream)
+    row0, rows = pipe.row0, pipe.rows
     wall, kernel_ms = time_frames(w, pipe, pitch, args.steps, args.warmup, stream)
     wall = max_over_ranks(wall)
     total_rays = WIDTH * height * args.steps
@@ -274,10 +240,12 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic: pinned 64-sphere cave (SURVEY 8d config 3), Floor.png texels",
             "config": {"workload": f"{WIDTH}x{height} lcg64 pose(0,0), {world_size} row band(s)"
-                                   + (" + RCCL gather to rank 0 (overlapped)" if world_size > 1 else ""),
+                                   + (" + RCCL transfer to rank 0 (overlapped, bands tuned)"
+                                      if world_size > 1 else ""),
                        "width": WIDTH, "height": height, "spheres": int(scene.spheres.shape[0]),
                        "parallelism": f"row-bands x{world_size}"},
             "kernel_ms": round(kernel_ms, 4),
+            "bands": bands,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None,

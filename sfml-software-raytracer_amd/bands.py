@@ -1,0 +1,204 @@
+"""Row bands of one frame over the GPUs of a node, gathered to rank 0.
+
+Pixels are independent (SphereWorld.cpp:94-110 reads nothing but the camera,
+the scene and (i, j)), so a frame splits into contiguous row bands, one per
+rank; each rank renders its band with GLOBAL row indices (sfrt_world_render_band),
+and the bands travel to rank 0 over RCCL -- the path's one exchange step.
+
+Two things shape the partition on MI355X:
+
+* rank 0's own band never crosses a link, every other band does.  A 4K
+  band renders at ~33 Grays/s (0.03 ns per pixel) but crosses one xGMI link
+  at 4 B per pixel (~0.06 ns per pixel at ~65 GB/s one way), so with equal
+  bands every rank but 0 idles on its link.  ``root_weighted_spans`` gives
+  rank 0 ``factor`` times the rows of each other rank;
+* the link/render ratio depends on the node (link generation, RCCL channel
+  count, clocks, the scene).  ``tune_spans`` times the real pipeline for a
+  few factors during warm-up and keeps the fastest (every rank takes the same
+  decision from the same all-reduced times).  Factor 1 is the plain equal
+  split with one RCCL gather.
+
+``BandPipeline`` double-buffers bands and frames so that the transfer of
+frame k overlaps the render of frame k + 1.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.distributed as dist
+
+ALIGN = 8  # rows per kernel tile: bands that start on a tile row waste no lanes
+
+# Root factors tried by tune_spans (1.0 = equal bands).
+DEFAULT_FACTORS = (1.0, 1.5, 2.0, 2.5, 3.0, 4.0)
+
+
+def band_of(rank: int, world: int, height: int) -> tuple[int, int]:
+    """Equal split: rank r renders rows [r*H/n, (r+1)*H/n)."""
+    r0 = rank * height // world
+    return r0, (rank + 1) * height // world - r0
+
+
+def equal_spans(height: int, world: int) -> list[tuple[int, int]]:
+    return [band_of(r, world, height) for r in range(world)]
+
+
+def root_weighted_spans(height: int, world: int, factor: float,
+                        align: int = ALIGN) -> list[tuple[int, int]]:
+    """(row0, rows) per rank: rank 0 renders about `factor` times the rows of every
+    other rank (their bands are equal and `align`-row multiples).  factor == 1, or a
+    frame too short to weight, gives the equal split."""
+    if world == 1:
+        return [(0, height)]
+    if factor == 1.0:
+        return equal_spans(height, world)
+    other = int(height / (world - 1 + factor))
+    other -= other % align
+    if other <= 0 or other * (world - 1) >= height:
+        return equal_spans(height, world)
+    first = height - (world - 1) * other
+    return [(0, first)] + [(first + (r - 1) * other, other) for r in range(1, world)]
+
+
+def check_spans(spans, height: int) -> None:
+    """Bands must tile [0, height) in rank order (rank 0 first)."""
+    row = 0
+    for r0, n in spans:
+        if r0 != row or n < 0:
+            raise ValueError(f"bands {spans} do not tile {height} rows")
+        row += n
+    if row != height:
+        raise ValueError(f"bands {spans} do not tile {height} rows")
+
+
+class BandPipeline:
+    """Row-band frames with the transfer to rank 0 overlapped with rendering.
+
+    Every rank owns `depth` band buffers; rank 0 also owns `depth` whole
+    frames.  Frame k renders into band k % depth and its transfer into frame
+    k % depth is queued asynchronously (RCCL runs it on its own stream after
+    the render that produced the band), so frame k+1 renders while frame k
+    crosses xGMI.  Reusing a buffer first waits (stream-side on RCCL) for the
+    transfer that last read it.  Equal bands use one gather collective;
+    unequal bands one batch of point-to-point transfers straight into the
+    frame's row slices.  With one rank the band IS the frame and nothing is
+    exchanged."""
+
+    def __init__(self, rank: int, world_size: int, height: int, pitch: int, device,
+                 depth: int = 2, spans=None):
+        self.rank, self.world_size, self.height = rank, world_size, height
+        self.spans = list(spans) if spans is not None else equal_spans(height, world_size)
+        check_spans(self.spans, height)
+        if len(self.spans) != world_size:
+            raise ValueError("one band per rank")
+        self.equal = len({n for _, n in self.spans}) == 1
+        self.depth = depth if world_size > 1 else 1
+        self.row0, self.rows = self.spans[rank]
+        self.frames, self.views = [], []
+        if world_size == 1:
+            self.frames = [torch.empty(height, pitch, dtype=torch.uint8, device=device)]
+            self.bands = self.frames
+        else:
+            if rank == 0:
+                for _ in range(self.depth):
+                    fr = torch.empty(height, pitch, dtype=torch.uint8, device=device)
+                    self.frames.append(fr)
+                    self.views.append([fr[r0:r0 + n] for r0, n in self.spans])
+            if rank == 0 and not self.equal:
+                # rank 0 renders straight into its rows of the frame (no copy)
+                self.bands = [v[0] for v in self.views]
+            else:
+                self.bands = [torch.empty(self.rows, pitch, dtype=torch.uint8, device=device)
+                              for _ in range(self.depth)]
+        self.pending = [[] for _ in range(self.depth)]
+
+    def acquire(self, k: int):
+        """The band buffer for frame k, once the transfer that last read it is done."""
+        b = k % self.depth
+        for work in self.pending[b]:
+            work.wait()
+        self.pending[b] = []
+        return self.bands[b]
+
+    def submit(self, k: int) -> None:
+        """Queue frame k's transfer (after everything already queued on the current stream)."""
+        if self.world_size == 1:
+            return
+        b = k % self.depth
+        band = self.bands[b]
+        views = self.views[b] if self.rank == 0 else None
+        if self.equal:
+            self.pending[b] = [dist.gather(band, views, dst=0, async_op=True)]
+        elif self.rank == 0:
+            ops = [dist.P2POp(dist.irecv, views[r], r) for r in range(1, self.world_size)
+                   if self.spans[r][1] > 0]
+            self.pending[b] = dist.batch_isend_irecv(ops) if ops else []
+        elif self.rows > 0:
+            self.pending[b] = dist.batch_isend_irecv([dist.P2POp(dist.isend, band, 0)])
+
+    def drain(self) -> None:
+        for b in range(self.depth):
+            for work in self.pending[b]:
+                work.wait()
+            self.pending[b] = []
+
+    def frame(self, k: int):
+        """Rank 0's assembled frame k (valid after drain() or the next acquire of its slot)."""
+        return self.frames[k % self.depth] if self.frames else None
+
+
+def max_over_ranks(x: float, device="cpu") -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def run_frames(pipe: BandPipeline, render, frames: int, sync=lambda: None) -> float:
+    """Render + transfer `frames` frames through `pipe`; wall seconds between two
+    barriers (this rank's view).  render(band_tensor, row0, rows) queues one band."""
+    if dist.is_initialized():
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(frames):
+        band = pipe.acquire(k)
+        render(band, pipe.row0, pipe.rows)
+        pipe.submit(k)
+    pipe.drain()
+    sync()
+    if dist.is_initialized():
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def tune_spans(render, rank: int, world_size: int, height: int, pitch: int, device,
+               factors=DEFAULT_FACTORS, frames: int = 8, warm: int = 2,
+               sync=lambda: None, reduce_device="cpu"):
+    """Pick the root factor whose pipelined frames run fastest on this node.
+
+    Every candidate partition runs `warm` + `frames` real frames through a
+    BandPipeline; the time that counts is the max over ranks (all-reduced, so
+    every rank sees the same numbers and takes the same decision).  Returns
+    (spans, factor, {factor: ms per frame})."""
+    if world_size == 1:
+        return [(0, height)], 1.0, {}
+    table, best = {}, None
+    tried = set()
+    for f in factors:
+        spans = root_weighted_spans(height, world_size, f)
+        key = tuple(spans)
+        if key in tried:
+            continue
+        tried.add(key)
+        pipe = BandPipeline(rank, world_size, height, pitch, device, spans=spans)
+        run_frames(pipe, render, warm, sync)
+        wall = max_over_ranks(run_frames(pipe, render, frames, sync), reduce_device)
+        del pipe
+        ms = wall / frames * 1e3
+        table[f] = round(ms, 4)
+        if best is None or ms < best[0]:
+            best = (ms, f, spans)
+    return best[2], best[1], table

@@ -1,11 +1,12 @@
 """Multi-rank row bands + gather (bench.py's N > 1 path) on CPU with gloo.
 
 Each rank renders its row band of the frame with the CPU restatement (this is
-test infrastructure standing in for the device fill), then bench.py's own
-BandPipeline (double-buffered bands, asynchronous gather / point-to-point
+test infrastructure standing in for the device fill), then the package's
+bands.BandPipeline (double-buffered bands, asynchronous gather / point-to-point
 transfers to rank 0) assembles the frames on rank 0, which must equal the
 single-rank frames byte for byte -- three frames with different camera poses
-in flight without draining in between.  world_size 2 and 3 (uneven bands).
+in flight without draining in between.  world_size 2 and 3, equal and
+root-weighted bands; the band tuner agrees across ranks.
 """
 import os
 import socket
@@ -25,11 +26,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world_size, port, width, height, out_path):
+def _worker(rank, world_size, port, width, height, out_path, factor=1.0):
     import sys
     for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), os.path.join(ROOT, "oracle"), ROOT):
         sys.path.insert(0, p)
-    import bench
+    import bands
     import oracle
     import scenes
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
@@ -39,7 +40,8 @@ def _worker(rank, world_size, port, width, height, out_path):
     poses = [(0.4, 0.05), (1.3, -0.2), (2.9, 0.3)]
     oracles = [oracle.Oracle.from_scene(scenes.lcg64().posed(*p), width, height, tex, tw, th)
                for p in poses]
-    pipe = bench.BandPipeline(rank, world_size, height, pitch, "cpu")
+    spans = bands.root_weighted_spans(height, world_size, factor)
+    pipe = bands.BandPipeline(rank, world_size, height, pitch, "cpu", spans=spans)
     for k, o in enumerate(oracles):
         band = pipe.acquire(k)
         band.copy_(torch.from_numpy(o.render_band(pipe.row0, pipe.rows).reshape(pipe.rows, pitch)))
@@ -53,22 +55,69 @@ def _worker(rank, world_size, port, width, height, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world_size,height", [(2, 90), (3, 100)])
-def test_row_band_gather_matches_single_rank(tmp_path, world_size, height):
+@pytest.mark.parametrize("world_size,height,factor", [(2, 90, 1.0), (3, 100, 1.0), (2, 90, 2.5),
+                                                      (3, 100, 1.5)])
+def test_row_band_gather_matches_single_rank(tmp_path, world_size, height, factor):
     out = str(tmp_path / "ok.npy")
-    mp.start_processes(_worker, args=(world_size, _free_port(), 160, height, out),
+    mp.start_processes(_worker, args=(world_size, _free_port(), 160, height, out, factor),
                        nprocs=world_size, start_method="spawn", join=True)
     assert bool(np.load(out)[0])
 
 
 def test_band_partition_covers_rows():
-    import bench
+    import bands
     for world_size in (1, 2, 3, 4, 8):
-        for height in (1, 7, 2160, 4320, 16384, 17280):
+        for height in (1, 7, 90, 2160, 4320, 16384, 17280):
             if height < world_size:
                 continue
-            spans = [bench.band_of(r, world_size, height) for r in range(world_size)]
-            assert spans[0][0] == 0
-            assert sum(n for _, n in spans) == height
-            for (a, n), (b, _) in zip(spans, spans[1:]):
-                assert a + n == b
+            for factor in (1.0,) + bands.DEFAULT_FACTORS + (0.5, 10.0):
+                spans = bands.root_weighted_spans(height, world_size, factor)
+                bands.check_spans(spans, height)
+                assert len(spans) == world_size
+                if spans != bands.equal_spans(height, world_size):
+                    # weighted: equal, tile-aligned bands on ranks 1.., rank 0 takes the rest
+                    others = {n for _, n in spans[1:]}
+                    assert len(others) == 1 and others.pop() % bands.ALIGN == 0
+                    assert spans[0][1] >= spans[1][1] or factor < 1.0
+    eq = bands.root_weighted_spans(17280, 8, 1.0)
+    assert eq == [(r * 2160, 2160) for r in range(8)]
+    w = bands.root_weighted_spans(17280, 8, 2.0)
+    assert w[1][1] == 1920 and w[0][1] == 17280 - 7 * 1920
+
+
+def _tune_worker(rank, world_size, port, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), ROOT):
+        sys.path.insert(0, p)
+    import time
+    import bands
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world_size)
+    height, pitch = 64, 16
+
+    def render(band, row0, rows):  # rows [row0, row0+rows) of a synthetic frame
+        band.copy_(torch.arange(row0, row0 + rows, dtype=torch.int64).remainder(251)
+                   .to(torch.uint8)[:, None].expand(rows, pitch))
+        time.sleep(1e-4 * rows if rank == 0 else 1e-5 * rows)
+
+    spans, factor, table = bands.tune_spans(render, rank, world_size, height, pitch, "cpu",
+                                            factors=(1.0, 2.0, 3.0), frames=3, warm=1)
+    got = torch.tensor([factor] + [float(n) for _, n in spans], dtype=torch.float64)
+    allv = [torch.zeros_like(got) for _ in range(world_size)]
+    dist.all_gather(allv, got)
+    pipe = bands.BandPipeline(rank, world_size, height, pitch, "cpu", spans=spans)
+    bands.run_frames(pipe, render, 2)
+    if rank == 0:
+        want = torch.arange(height).remainder(251).to(torch.uint8)[:, None].expand(height, pitch)
+        same = all(torch.equal(a, allv[0]) for a in allv)
+        np.save(out_path, np.array([same, torch.equal(pipe.frame(1), want), len(table) == 3]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tune_spans_agrees_across_ranks(tmp_path):
+    """Every rank picks the same partition, and the tuned pipeline assembles the frame."""
+    out = str(tmp_path / "tune.npy")
+    mp.start_processes(_tune_worker, args=(3, _free_port(), out), nprocs=3,
+                       start_method="spawn", join=True)
+    assert np.load(out).all()
