@@ -49,7 +49,7 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
 // Shading tail, SphereWorld.cpp:373-381.  Returns RGBA8 packed (r in byte 0).
 __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d, float px,
                                          float py, float pz, PixelDump* dump) {
-  float ang = d.atan_c - sfrt_math::atan2f(pz, px);
+  float ang = d.atan_c - atan2f_wave(pz, px);  // == sfrt_math::atan2f (sfrt_device.h)
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
   const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
   const float ex = px - d.cx, ey = py - d.cy, ez = pz - d.cz;
@@ -399,12 +399,12 @@ __device__ __forceinline__ void trace_tile(const FrameRec& f, const SphereRec* _
 // marching lanes, [min over marching lanes, max over all lanes] of tacc.
 // Lanes only move forward, so a sphere left behind by every marching lane is
 // never needed again and one not yet reached is not needed yet.
-template <int SLOTS>
+template <int SLOTS, int WPB, int TLO_EVERY = 1>
 __device__ __forceinline__ void trace_tile_window(const FrameRec& f,
                                                   const SphereRec* __restrict__ sph) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x * kWavesPerBlock + wave;
+  const int wave = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
+  const int tile = blockIdx.x * WPB + wave;
   const int tile_y = tile / f.tiles_x;
   const int tile_x = tile - tile_y * f.tiles_x;
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
@@ -490,13 +490,16 @@ __device__ __forceinline__ void trace_tile_window(const FrameRec& f,
     }
   } else {
     bool full = !windowed;
+    float tlo = 0.0f;
     while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
       if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
       uint64_t win = all;
       if (!full) {
-        // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32)
-        const float tlo = __uint_as_float(
-            wave_min_u32(__float_as_uint(mv > 0.0f ? tacc : __builtin_inff())));
+        // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32).  The
+        // low end only rises, so an earlier value is a valid lower bound
+        // (refreshed every TLO_EVERY steps, as trace_tile_window_r).
+        if (TLO_EVERY == 1 || trips % TLO_EVERY == 1)
+          tlo = __uint_as_float(wave_min_u32(__float_as_uint(mv > 0.0f ? tacc : __builtin_inff())));
         const float thi = __uint_as_float(wave_max_u32(__float_as_uint(tacc)));
         win = m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
       }
@@ -564,6 +567,8 @@ __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int t
 }
 
 // Pass bodies of one sphere for the lane's R rays under one scalar branch.
+// (Lane-masked selects through inline asm instead of these exec-masked
+// updates were measured slower: 1% at R = 2, 15% at R = 1.)
 template <int R>
 __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, float rad, int k,
                                             float (&L)[R], int (&dnew)[R]) {
@@ -600,12 +605,12 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
   }
 }
 
-template <int SLOTS, int R>
+template <int SLOTS, int R, int WPB, int TLO_EVERY = 1>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
                                                     const SphereRec* __restrict__ sph) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x * kWavesPerBlock + wave;
+  const int wave = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
+  const int tile = blockIdx.x * WPB + wave;
   const int tile_y = tile / f.tiles_x;  // f.tiles_x = ceil(sub_w / (8 R)) for this kernel
   const int tile_x = tile - tile_y * f.tiles_x;
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
@@ -632,11 +637,16 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     tacc[r] = l0;
     marching = marching || mv[r] > 0.0f;
   }
+  // mv >= +0 always (0, or the last step length), so "marching" is mv's bits != 0:
+  // an integer compare straight into a lane mask
+  auto marching_mask = [&](int r) {
+    return __builtin_amdgcn_ballot_w64(__float_as_uint(mv[r]) != 0u);
+  };
   auto any_marching = [&]() {
-    bool q = false;
+    uint64_t q = 0;
 #pragma unroll
-    for (int r = 0; r < R; r++) q = q || mv[r] > 0.0f;
-    return __builtin_amdgcn_ballot_w64(q) != 0;
+    for (int r = 0; r < R; r++) q |= marching_mask(r);
+    return q != 0;
   };
   const uint64_t all = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
   const bool windowed = f.cull && __builtin_amdgcn_ballot_w64(marching) != 0;
@@ -646,6 +656,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     const Cone cone = tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
     m = cull_window(f, sph, 0, cone, lo, hi);
   }
+  // pos += dir * L for marching rays (SphereWorld.cpp:371)
   auto advance = [&](const float (&L)[R], const int (&dnew)[R]) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -685,7 +696,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       }
     }
     uint64_t rest = 0;
-    while (any_marching()) {
+    // single-exit loop (the march guard is part of the condition): a second
+    // exit makes the compiler shuffle every loop-carried register each step
+    for (; any_marching() && trips < kMaxIterations; ++trips) {
       if (trips == kCullSafeIterations) {
 #pragma unroll
         for (int q = 0; q < SLOTS; q++) ssp[q] = 0.0f;
@@ -703,26 +716,33 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
       }
       advance(L, dnew);
-      if (++trips >= kMaxIterations) {
-        if (any_marching() && lane == 0) atomicOr(f.status, 1);
-        break;
-      }
     }
   } else {
     bool full = !windowed;
-    while (any_marching()) {
+    float tlo = 0.0f;
+    for (; any_marching() && trips < kMaxIterations; ++trips) {
       if (trips == kCullSafeIterations) full = true;
       uint64_t win = all;
       if (!full) {
-        uint32_t tl = 0x7f800000u, th = 0u;  // +inf, +0
+        uint32_t th = 0u;  // +0
 #pragma unroll
         for (int r = 0; r < R; r++) {
           const uint32_t u = __float_as_uint(tacc[r]);
-          const uint32_t ua = mv[r] > 0.0f ? u : 0x7f800000u;
-          tl = ua < tl ? ua : tl;
           th = u > th ? u : th;
         }
-        const float tlo = __uint_as_float(wave_min_u32(tl));
+        // The low end only rises (rays move forward and leave the march), so a
+        // value from an earlier step is a valid lower bound: refreshed every
+        // TLO_EVERY steps.
+        if (TLO_EVERY == 1 || trips % TLO_EVERY == 1) {
+          uint32_t tl = 0x7f800000u;  // +inf
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            const uint32_t u = __float_as_uint(tacc[r]);
+            const uint32_t ua = mv[r] > 0.0f ? u : 0x7f800000u;
+            tl = ua < tl ? ua : tl;
+          }
+          tlo = __uint_as_float(wave_min_u32(tl));
+        }
         const float thi = __uint_as_float(wave_max_u32(th));
         win = m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
       }
@@ -736,12 +756,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
       }
       advance(L, dnew);
-      if (++trips >= kMaxIterations) {
-        if (any_marching() && lane == 0) atomicOr(f.status, 1);
-        break;
-      }
     }
   }
+  if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (valid[r]) {
@@ -752,14 +769,14 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   }
 }
 
-template <int SLOTS, int R>
-__global__ __launch_bounds__(256) void k_trace_window_r(InlineArgs args) {
-  trace_tile_window_r<SLOTS, R>(args.f, args.s);
+template <int SLOTS, int R, int WPB = kWavesPerBlock, int TLO_EVERY = 1>
+__global__ __launch_bounds__(64 * WPB) void k_trace_window_r(InlineArgs args) {
+  trace_tile_window_r<SLOTS, R, WPB, TLO_EVERY>(args.f, args.s);
 }
 
-template <int SLOTS>
-__global__ __launch_bounds__(256) void k_trace_window(InlineArgs args) {
-  trace_tile_window<SLOTS>(args.f, args.s);
+template <int SLOTS, int WPB = kWavesPerBlock, int TLO_EVERY = 1>
+__global__ __launch_bounds__(64 * WPB) void k_trace_window(InlineArgs args) {
+  trace_tile_window<SLOTS, WPB, TLO_EVERY>(args.f, args.s);
 }
 
 template <int SLOTS, bool REST_LDS>
@@ -923,40 +940,54 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
   const long long tiles = tiles_y * f.tiles_x;
   if (tiles <= 0) return 0;
   const long long blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (blocks > 0x7fffffffLL) return -1;
+  if (blocks > 0x7fffffffLL || tiles > 0x7fffffffLL) return -1;
   hipStream_t s = (hipStream_t)stream;
   // Default for n <= 64: 16x8 tiles (two pixels per lane) once the scene has
   // more than kPairMinSpheres spheres; with few spheres the 8x8 kernel's
-  // tighter tiles win (measured).
-  const int rays = f.variant == 40 || f.variant == 41 ? 2
+  // tighter tiles win.  Both default kernels run one wave per workgroup (a
+  // finished wave's slot is refilled at once) and the pair kernel refreshes
+  // the march window's low end every second step (measured).
+  const int rays = f.variant == 49 ? 1
+                   : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
                    : f.variant == 42 ? 3
                    : f.variant == 43 ? 4
                    : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
-  if (f.n <= kInlineSpheres && rays > 1) {
+  if (f.n <= kInlineSpheres && (rays > 1 || f.variant == 49)) {
     // (8 rays) x 8 tiles: several pixels per lane
     InlineArgs args;
     args.f = f;
     args.f.tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    const dim3 g2((unsigned)((tiles_y * args.f.tiles_x + kWavesPerBlock - 1) / kWavesPerBlock));
-    if (f.variant == 41)
-      hipLaunchKernelGGL((k_trace_window_r<0, 2>), g2, dim3(256), 0, s, args);
-    else if (rays == 3)
-      hipLaunchKernelGGL((k_trace_window_r<kSlots, 3>), g2, dim3(256), 0, s, args);
-    else if (rays == 4)
-      hipLaunchKernelGGL((k_trace_window_r<kSlots, 4>), g2, dim3(256), 0, s, args);
-    else
-      hipLaunchKernelGGL((k_trace_window_r<kSlots, 2>), g2, dim3(256), 0, s, args);
+    const long long tiles2 = tiles_y * args.f.tiles_x;
+    const dim3 g1((unsigned)tiles2), b1(64);  // one wave per workgroup
+    const dim3 g4((unsigned)((tiles2 + kWavesPerBlock - 1) / kWavesPerBlock)), b4(256);
+    // SFRT_OPT_VARIANT (A/B only): 40 / 41: four waves per workgroup, low end every
+    // step, 4 / 0 slots; 42 / 43: 24x8 / 32x8 tiles; 44 / 45: one / two waves per
+    // workgroup, low end every step; 48: low end every 4th step; 49: 8x8 tiles here
+    switch (f.variant) {
+      case 40: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2>), g4, b4, 0, s, args); break;
+      case 41: hipLaunchKernelGGL((k_trace_window_r<0, 2>), g4, b4, 0, s, args); break;
+      case 42: hipLaunchKernelGGL((k_trace_window_r<kSlots, 3>), g4, b4, 0, s, args); break;
+      case 43: hipLaunchKernelGGL((k_trace_window_r<kSlots, 4>), g4, b4, 0, s, args); break;
+      case 44: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1>), g1, b1, 0, s, args); break;
+      case 45:
+        hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 2>), dim3((unsigned)((tiles2 + 1) / 2)),
+                           dim3(128), 0, s, args);
+        break;
+      case 48: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 4>), g1, b1, 0, s, args); break;
+      case 49: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2>), g1, b1, 0, s, args); break;
+      case 47:
+      default: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2>), g1, b1, 0, s, args); break;
+    }
   } else if (f.n <= kInlineSpheres) {
     InlineArgs args;
     args.f = f;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    // SFRT_OPT_VARIANT (tuning A/B only).  Default (8x8 tiles): march window
-    // with the SGPR-slot march for waves with <= kSlots culled spheres; 35:
-    // that kernel whatever n; 40/41: the 16x8 pair kernel with 4/0 slots;
-    // 42/43: 24x8 / 32x8 tiles (3 / 4 pixels per lane);
-    // 2: slots + the rest every step (no window); 1/6/8: slot counts; 16/17:
-    // LDS-backed rest; 32/36: window with 0/6 slots.
+    // SFRT_OPT_VARIANT (tuning A/B only).  Default (8x8 tiles, one wave per
+    // workgroup, window low end every second step): march window with the
+    // SGPR-slot march for waves with <= kSlots culled spheres; 52: the same
+    // whatever n; 46: low end every step; 35: also four waves per workgroup; 2: slots + the rest every step (no window); 1/6/8: slot
+    // counts; 16/17: LDS-backed rest; 32/36: window with 0/6 slots.
     const dim3 g((unsigned)blocks), b(256);
     switch (f.variant) {
       case 1: hipLaunchKernelGGL((k_trace_inline<0, false>), g, b, 0, s, args); break;
@@ -967,8 +998,14 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
       case 2: hipLaunchKernelGGL((k_trace_inline<kSlots, false>), g, b, 0, s, args); break;
       case 32: hipLaunchKernelGGL(k_trace_window<0>, g, b, 0, s, args); break;
       case 36: hipLaunchKernelGGL(k_trace_window<6>, g, b, 0, s, args); break;
-      case 35:
-      default: hipLaunchKernelGGL(k_trace_window<kSlots>, g, b, 0, s, args); break;
+      case 35: hipLaunchKernelGGL(k_trace_window<kSlots>, g, b, 0, s, args); break;
+      case 46:
+        hipLaunchKernelGGL((k_trace_window<kSlots, 1>), dim3((unsigned)tiles), dim3(64), 0, s, args);
+        break;
+      case 52:
+      default:
+        hipLaunchKernelGGL((k_trace_window<kSlots, 1, 2>), dim3((unsigned)tiles), dim3(64), 0, s, args);
+        break;
     }
   } else {
     if (f.variant == 2) {  // A/B: the per-word culled lists visited every step

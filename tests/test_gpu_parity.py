@@ -95,7 +95,7 @@ def test_cull_on_off_identical(world, floor):
     assert diff_report(a, b, 3840) == ""
 
 
-@pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 35, 36, 40, 41, 42, 43])
+@pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 35, 36, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 52])
 def test_kernel_variants_identical(world, floor, variant):
     """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
     produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
@@ -260,7 +260,7 @@ def test_errors_fail_loudly(world):
 
 
 @pytest.mark.parametrize("fn,arg", [("asinf", "1"), ("atanf", "1"), ("atan2f", "100000000"),
-                                    ("sqrt_div", "16"), ("divpi", "1"), ("atan2f_x1", "1"),
+                                    ("sqrt_div", "16"), ("divpi", "1"), ("atan2f_x1", "1"), ("atan2f_wave", "400000000"),
                                     ("acosf", "1")])
 def test_device_math_matches_libm(fn, arg, tmp_path):
     """sfrt_math on gfx950 vs host glibc: every binary32 input (atanf, asinf)."""
