@@ -245,8 +245,8 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
 // loads (wave-uniform addresses, scalar cache).  Variant 1 stages them in LDS
 // instead (one copy per workgroup); measured slower on MI355X
 // (profiles/r1_glsl_variants.json), kept for A/B.
-template <bool LDS>
-__global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
+template <bool LDS, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) void k_glsl(GlslFrame f) {
   __shared__ GlslWall s_walls[LDS ? kGlslMax : 1];
   __shared__ GlslBall s_balls[LDS ? kGlslMax : 1];
   if (LDS) {
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tile = blockIdx.x * WPB + (WPB == 1 ? 0 : (int)(threadIdx.x >> 6));
   const int tx = tile % f.tiles_x, ty = tile / f.tiles_x;
   const int i = tx * 8 + (lane & 7);
   const int r = ty * 8 + (lane >> 3);
@@ -272,6 +272,8 @@ int launch_glsl(const GlslFrame& f, void* stream) {
   const dim3 g((unsigned)((tiles + 3) / 4)), b(256);
   if (f.variant == 1)
     hipLaunchKernelGGL(k_glsl<true>, g, b, 0, (hipStream_t)stream, f);
+  else if (f.variant == 2)  // one wave per workgroup (measured equal to four)
+    hipLaunchKernelGGL((k_glsl<false, 1>), dim3((unsigned)tiles), dim3(64), 0, (hipStream_t)stream, f);
   else
     hipLaunchKernelGGL(k_glsl<false>, g, b, 0, (hipStream_t)stream, f);
   return hipGetLastError() != hipSuccess;

@@ -253,10 +253,16 @@ __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_
   return raycast_t<true>(f, dir, yscale, atan_dir);
 }
 
-// 16x16 pixels per 256-thread workgroup.
-__global__ __launch_bounds__(256) void k_voxel(VoxFrame f) {
-  const int a = blockIdx.x * 16 + (threadIdx.x & 15);
-  const int b = f.sub_row0 + blockIdx.y * 16 + (threadIdx.x >> 4);
+// 8x8 pixels per one-wave workgroup (a finished wave's slot refills at once;
+// 0.7-1.5% faster than 16x16 per 256 threads, which -DSFRT_VOXEL_TILE16 restores).
+#ifdef SFRT_VOXEL_TILE16
+constexpr int kVoxTile = 16;
+#else
+constexpr int kVoxTile = 8;
+#endif
+__global__ __launch_bounds__(kVoxTile * kVoxTile) void k_voxel(VoxFrame f) {
+  const int a = blockIdx.x * kVoxTile + (threadIdx.x % kVoxTile);
+  const int b = f.sub_row0 + blockIdx.y * kVoxTile + (threadIdx.x / kVoxTile);
   if (a >= f.sub_w || b >= f.sub_row0 + f.sub_rows) return;
   const int i = f.xstart + a * f.xadd;
   const int j = f.ystart + b * f.yadd;
@@ -269,8 +275,9 @@ __global__ __launch_bounds__(256) void k_voxel(VoxFrame f) {
 
 int launch_voxel(const VoxFrame& f, void* stream) {
   if (f.sub_w <= 0 || f.sub_rows <= 0) return 0;
-  const dim3 grid((unsigned)((f.sub_w + 15) / 16), (unsigned)((f.sub_rows + 15) / 16));
-  hipLaunchKernelGGL(k_voxel, grid, dim3(256), 0, (hipStream_t)stream, f);
+  const dim3 grid((unsigned)((f.sub_w + kVoxTile - 1) / kVoxTile),
+                  (unsigned)((f.sub_rows + kVoxTile - 1) / kVoxTile));
+  hipLaunchKernelGGL(k_voxel, grid, dim3(kVoxTile * kVoxTile), 0, (hipStream_t)stream, f);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
