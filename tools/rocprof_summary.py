@@ -27,7 +27,7 @@ import re
 
 def pixels_per_thread(kernel_name: str) -> int:
     """Pixels one work-item writes: R for k_trace_window_r<SLOTS, R>, else 1."""
-    m = re.search(r"k_trace_window_r<\s*\d+\s*,\s*(\d+)\s*>", kernel_name)
+    m = re.search(r"k_trace_window_r<\s*\d+\s*,\s*(\d+)", kernel_name)
     return int(m.group(1)) if m else 1
 
 
