@@ -337,3 +337,69 @@ def test_pipelined_frames_match_update_image(world, floor):
         assert diff_report(frames[kk % 3].array, world.render(), width) == "", kk
     for fr in frames:
         fr.free()
+
+
+def _fuzz_scene(seed):
+    """A random scene/camera/frame: sphere counts on both sides of every kernel switch
+    (8x8 vs pair kernel at 16, inline vs global at 64), caller (unsorted) order, cameras
+    inside, outside, at a centre or near a surface, any pose and field of view."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([1, 2, 3, 7, 16, 17, 33, 64, 65, 130]))
+    scale = float(rng.choice([5.0, 20.0, 60.0]))
+    c = rng.uniform(-scale, scale, size=(n, 3))
+    if rng.random() < 0.5:
+        c = np.round(c)  # the reference's rand() scenes have integer centres
+    r = rng.uniform(0.05, scale / 2, size=(n, 1))
+    spheres = np.concatenate([c, r], axis=1).astype(np.float32)
+    mode = int(rng.integers(4))
+    k = int(rng.integers(n))
+    if mode == 0:
+        cam = spheres[k, :3]                                   # at a centre
+    elif mode == 1:
+        cam = spheres[k, :3] + rng.uniform(-0.5, 0.5, 3) * spheres[k, 3]  # inside
+    elif mode == 2:
+        d = rng.normal(size=3)
+        cam = spheres[k, :3] + d / np.linalg.norm(d) * spheres[k, 3] * 0.999  # near the surface
+    else:
+        cam = rng.uniform(-2 * scale, 2 * scale, 3)            # anywhere (often outside)
+    cam = tuple(float(x) for x in np.asarray(cam, dtype=np.float32))
+    fov = (None, None) if rng.random() < 0.5 else (float(np.float32(rng.uniform(0.2, 1.5))),
+                                                   float(np.float32(rng.uniform(0.2, 1.2))))
+    sc = scenes.Scene(f"fuzz{seed}", spheres, cam_pos=cam,
+                      rotation=float(np.float32(rng.uniform(-7, 7))),
+                      hrotation=float(np.float32(rng.uniform(-1.5, 1.5))))
+    if fov[0] is not None:
+        sc.fov_h, sc.fov_v = np.float32(fov[0]), np.float32(fov[1])
+    width, height = [(160, 90), (97, 61), (256, 8), (64, 200), (333, 41)][int(rng.integers(5))]
+    return sc, width, height
+
+
+@pytest.mark.parametrize("chunk", range(4))
+def test_random_scenes_match_oracle(world, floor, chunk):
+    """400 random scenes (100 per chunk) through the default kernels vs the oracle:
+    culling, march windows and both tile shapes must never change a byte."""
+    for seed in range(chunk * 100, chunk * 100 + 100):
+        sc, width, height = _fuzz_scene(seed)
+        world.set_scene(sc, width, height)
+        got = world.render()
+        want = oracle_for(sc, width, height, floor).render(host_threads())
+        msg = diff_report(got, want, width)
+        assert not msg, f"seed {seed} ({sc.spheres.shape[0]} spheres, cam {sc.cam_pos}, " \
+                        f"{width}x{height}): {msg}"
+
+
+def test_random_subsets_match_oracle(world, floor):
+    """UpdateImage(ystart, yadd, xstart, xadd) pixel subsets of random scenes (SphereWorld.cpp:94,97),
+    on a poisoned canvas: the same bytes as the oracle's, and no other byte touched."""
+    rng = np.random.default_rng(77)
+    for seed in range(60):
+        sc, width, height = _fuzz_scene(400 + seed)
+        yadd, xadd = int(rng.integers(1, 9)), int(rng.integers(1, 5))
+        ystart, xstart = int(rng.integers(0, yadd + 2)), int(rng.integers(0, xadd + 2))
+        world.set_scene(sc, width, height)
+        got = np.full(width * height * 4, 0xA5, dtype=np.uint8)
+        world.update_image(got, ystart, yadd, xstart, xadd)
+        want = np.full(width * height * 4, 0xA5, dtype=np.uint8)
+        oracle_for(sc, width, height, floor).update_image(want, ystart, yadd, xstart, xadd)
+        msg = diff_report(got, want, width)
+        assert not msg, f"seed {seed} subset ({ystart},{yadd},{xstart},{xadd}): {msg}"
