@@ -207,6 +207,14 @@ __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereR
   return __builtin_amdgcn_ballot_w64(inc);
 }
 
+// std::max(largestDist, t) (SphereWorld.cpp:367) for L >= +0 and t > 0.01f
+// (the pass test), both finite: their bit patterns order like the values, so
+// one v_max_u32 gives the compare-select's bits (v_max_f32 would first
+// canonicalise the loop-carried L).
+__device__ __forceinline__ float max_nonneg(float L, float t) {
+  return __uint_as_float(__builtin_elementwise_max(__float_as_uint(L), __float_as_uint(t)));
+}
+
 // Pass body of a sphere test (SphereWorld.cpp:366-368) for the lanes in
 // `pass`: t = r - sqrtf(ss) exactly; largestDist = max; drawSphere = k.
 __device__ __forceinline__ void pass_body(bool pass, float ss, float r, int k, float& L,
@@ -223,12 +231,12 @@ __device__ __forceinline__ void pass_body(bool pass, float ss, float r, int k, f
     if ((__builtin_amdgcn_ballot_w64(ss < kTinySqrtArg) & pm) == 0) {
       if (pass) {
         const float t = r - sqrt_cr_normal(ss);
-        L = L < t ? t : L;  // std::max(largestDist, t)
+        L = max_nonneg(L, t);
         dnew = k;
       }
     } else if (pass) {
       const float t = r - __builtin_sqrtf(ss);
-      L = L < t ? t : L;
+      L = max_nonneg(L, t);
       dnew = k;
     }
   }
@@ -588,7 +596,7 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
       for (int r = 0; r < R; r++) {
         if (ss[r] < s_pass) {
           const float t = rad - sqrt_cr_normal(ss[r]);
-          L[r] = L[r] < t ? t : L[r];
+          L[r] = max_nonneg(L[r], t);
           dnew[r] = k;
         }
       }
@@ -597,7 +605,7 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
       for (int r = 0; r < R; r++) {
         if (ss[r] < s_pass) {
           const float t = rad - __builtin_sqrtf(ss[r]);
-          L[r] = L[r] < t ? t : L[r];
+          L[r] = max_nonneg(L[r], t);
           dnew[r] = k;
         }
       }
@@ -605,7 +613,16 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
   }
 }
 
-template <int SLOTS, int R, int WPB, int TLO_EVERY = 1>
+// FL (A/B flags): kFlMask -- marching masks from a plain f32 compare; kFlFree --
+// the advance runs on every lane (exact, see below) and edge lanes march as the
+// duplicates they are; kFlPrefetch -- the next visited record is loaded before
+// the current visit's arithmetic.
+// kFlPair -- visits taken two at a time: both records loaded, both spheres'
+// distances computed (four independent chains per lane), then the two pass
+// bodies in index order.
+constexpr int kFlMask = 1, kFlFree = 2, kFlPrefetch = 4, kFlPair = 8;
+
+template <int SLOTS, int R, int WPB, int TLO_EVERY = 1, int FL = 0>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
                                                     const SphereRec* __restrict__ sph) {
   const int lane = threadIdx.x & 63;
@@ -633,13 +650,14 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     py[r] = f.cam[1] + dy[r] * l0;
     pz[r] = f.cam[2] + dz[r] * l0;
     draw[r] = f.first_draw;
-    mv[r] = (valid[r] && l0 > 0.0f) ? 1.0f : 0.0f;
+    mv[r] = ((FL & kFlFree) || valid[r]) && l0 > 0.0f ? 1.0f : 0.0f;
     tacc[r] = l0;
     marching = marching || mv[r] > 0.0f;
   }
   // mv >= +0 always (0, or the last step length), so "marching" is mv's bits != 0:
   // an integer compare straight into a lane mask
   auto marching_mask = [&](int r) {
+    if (FL & kFlMask) return __builtin_amdgcn_ballot_w64(mv[r] > 0.0f);
     return __builtin_amdgcn_ballot_w64(__float_as_uint(mv[r]) != 0u);
   };
   auto any_marching = [&]() {
@@ -656,11 +674,16 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     const Cone cone = tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
     m = cull_window(f, sph, 0, cone, lo, hi);
   }
-  // pos += dir * L for marching rays (SphereWorld.cpp:371)
+  // pos += dir * L for marching rays (SphereWorld.cpp:371).  kFlFree: on every
+  // lane.  A ray that stopped had no passing sphere at its position (its last
+  // step visited every sphere that could pass), its position no longer moves,
+  // so each later step again has none: L = +0, dnew = draw, tacc + 0 = tacc,
+  // and p + d * (+0) = p -- also for p = -0, which a marching wave's ray only
+  // reaches through -0 + d * l0 with d of negative sign, so d * (+0) = -0.
   auto advance = [&](const float (&L)[R], const int (&dnew)[R]) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      if (mv[r] > 0.0f) {
+      if ((FL & kFlFree) || mv[r] > 0.0f) {
         px[r] = px[r] + dx[r] * L[r];
         py[r] = py[r] + dy[r] * L[r];
         pz[r] = pz[r] + dz[r] * L[r];
@@ -750,10 +773,46 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       int dnew[R];
 #pragma unroll
       for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
-      for (uint64_t mm = win; mm; mm &= mm - 1) {
-        const int k = __builtin_ctzll(mm);
-        const SphereRec& s = sph[k];
-        visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      if (FL & kFlPair) {
+        for (uint64_t mm = win; mm;) {
+          const int k1 = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          const SphereRec& s1 = sph[k1];
+          if (mm) {
+            const int k2 = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const SphereRec& s2 = sph[k2];
+            float ss1[R], ss2[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+              ss1[r] = dist2(px[r], py[r], pz[r], s1.cx, s1.cy, s1.cz);
+              ss2[r] = dist2(px[r], py[r], pz[r], s2.cx, s2.cy, s2.cz);
+            }
+            pass_body_r<R>(ss1, s1.s_pass, s1.r, k1, L, dnew);
+            pass_body_r<R>(ss2, s2.s_pass, s2.r, k2, L, dnew);
+          } else {
+            visit(s1.cx, s1.cy, s1.cz, s1.r, s1.s_pass, k1, L, dnew);
+          }
+        }
+      } else if (FL & kFlPrefetch) {
+        if (win) {
+          int k = __builtin_ctzll(win);
+          float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
+          for (uint64_t mm = win & (win - 1);; mm &= mm - 1) {
+            const int kn = mm ? __builtin_ctzll(mm) : k;
+            const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
+                        nsp = sph[kn].s_pass;
+            visit(cx, cy, cz, rad, sp, k, L, dnew);
+            if (!mm) break;
+            k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
+          }
+        }
+      } else {
+        for (uint64_t mm = win; mm; mm &= mm - 1) {
+          const int k = __builtin_ctzll(mm);
+          const SphereRec& s = sph[k];
+          visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+        }
       }
       advance(L, dnew);
     }
@@ -769,9 +828,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   }
 }
 
-template <int SLOTS, int R, int WPB = kWavesPerBlock, int TLO_EVERY = 1>
+template <int SLOTS, int R, int WPB = kWavesPerBlock, int TLO_EVERY = 1, int FL = 0>
 __global__ __launch_bounds__(64 * WPB) void k_trace_window_r(InlineArgs args) {
-  trace_tile_window_r<SLOTS, R, WPB, TLO_EVERY>(args.f, args.s);
+  trace_tile_window_r<SLOTS, R, WPB, TLO_EVERY, FL>(args.f, args.s);
 }
 
 template <int SLOTS, int WPB = kWavesPerBlock, int TLO_EVERY = 1>
@@ -942,17 +1001,23 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
   const long long blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > 0x7fffffffLL || tiles > 0x7fffffffLL) return -1;
   hipStream_t s = (hipStream_t)stream;
-  // Default for n <= 64: 16x8 tiles (two pixels per lane) once the scene has
-  // more than kPairMinSpheres spheres; with few spheres the 8x8 kernel's
-  // tighter tiles win.  Both default kernels run one wave per workgroup (a
-  // finished wave's slot is refilled at once) and the pair kernel refreshes
-  // the march window's low end every second step (measured).
+  // Default for n <= 64: trace_tile_window_r with 16x8 tiles (two pixels per
+  // lane) once the scene has more than kPairMinSpheres spheres; with few
+  // spheres 8x8 tiles (one pixel per lane) win.  Both run one wave per
+  // workgroup (a finished wave's slot is refilled at once), refresh the march
+  // window's low end every second step and use kFlMask | kFlFree (measured,
+  // DESIGN.md 5).
   const int rays = f.variant == 49 ? 1
                    : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
+                   : f.variant == 72 ? 3
+                   : f.variant == 73 ? 4
+                   : f.variant == 74 || f.variant == 75 ? 1
+                   : f.variant >= 60 && f.variant <= 71 ? 2
                    : f.variant == 42 ? 3
                    : f.variant == 43 ? 4
                    : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
-  if (f.n <= kInlineSpheres && (rays > 1 || f.variant == 49)) {
+  if (f.n <= kInlineSpheres &&
+      (rays > 1 || f.variant == 0 || f.variant == 49 || f.variant == 74 || f.variant == 75)) {
     // (8 rays) x 8 tiles: several pixels per lane
     InlineArgs args;
     args.f = f;
@@ -963,7 +1028,10 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     const dim3 g4((unsigned)((tiles2 + kWavesPerBlock - 1) / kWavesPerBlock)), b4(256);
     // SFRT_OPT_VARIANT (A/B only): 40 / 41: four waves per workgroup, low end every
     // step, 4 / 0 slots; 42 / 43: 24x8 / 32x8 tiles; 44 / 45: one / two waves per
-    // workgroup, low end every step; 48: low end every 4th step; 49: 8x8 tiles here
+    // workgroup, low end every step; 48: low end every 4th step; 49: 8x8 tiles here;
+    // 47: the default without FL flags; 61-71: 60 + FL bits (kFlMask 1, kFlFree 2,
+    // kFlPrefetch 4, kFlPair 8); 72 / 73 / 74: 24x8 / 32x8 / 8x8 tiles with the
+    // default flags, 75: 8x8 with kFlPair.  Measured: DESIGN.md 5.
     switch (f.variant) {
       case 40: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2>), g4, b4, 0, s, args); break;
       case 41: hipLaunchKernelGGL((k_trace_window_r<0, 2>), g4, b4, 0, s, args); break;
@@ -976,8 +1044,25 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
         break;
       case 48: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 4>), g1, b1, 0, s, args); break;
       case 49: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2>), g1, b1, 0, s, args); break;
-      case 47:
-      default: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2>), g1, b1, 0, s, args); break;
+      case 61: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 1>), g1, b1, 0, s, args); break;
+      case 62: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 2>), g1, b1, 0, s, args); break;
+      case 64: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 4>), g1, b1, 0, s, args); break;
+      case 67: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 7>), g1, b1, 0, s, args); break;
+      case 71: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 11>), g1, b1, 0, s, args); break;
+      case 72: hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 2, 3>), g1, b1, 0, s, args); break;
+      case 73: hipLaunchKernelGGL((k_trace_window_r<kSlots, 4, 1, 2, 3>), g1, b1, 0, s, args); break;
+      case 74:
+        hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlMask | kFlFree>), g1, b1, 0, s, args);
+        break;
+      case 75: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, 11>), g1, b1, 0, s, args); break;
+      case 47: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2>), g1, b1, 0, s, args); break;
+      case 63:
+      default:
+        if (rays == 1)  // default for n <= kPairMinSpheres: 8x8 tiles (= variant 74)
+          hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlMask | kFlFree>), g1, b1, 0, s, args);
+        else
+          hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlMask | kFlFree>), g1, b1, 0, s, args);
+        break;
     }
   } else if (f.n <= kInlineSpheres) {
     InlineArgs args;
