@@ -1,6 +1,6 @@
 """Summarise rocprofv3 CSV output of bench.py runs into profiles/.
 
-    python tools/rocprof_summary.py --trace DIR --fetch DIR --write DIR --tag r1 [--sq DIR]
+    python tools/rocprof_summary.py --trace DIR --fetch DIR --write DIR --tag r1 [--sq DIR ...]
                                     [--kernel k_trace|k_glsl|k_voxel] [--out profiles]
 
 Writes
@@ -41,7 +41,8 @@ def main():
     ap.add_argument("--trace", required=True)
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--sq", help="--pmc pass with SQ_INSTS_VALU / SQ_WAVES")
+    ap.add_argument("--sq", nargs="*", default=[],
+                    help="--pmc passes with SQ_* counters (SQ_INSTS_VALU / SQ_WAVES, stall counters)")
     ap.add_argument("--tag", required=True)
     ap.add_argument("--kernel", default="k_trace", help="kernel-name substring (k_trace, k_glsl, k_voxel)")
     ap.add_argument("--out", default="profiles")
@@ -67,9 +68,9 @@ def main():
                 acc[px].append(float(r["Counter_Value"]) * 1024.0)
         for grid, v in acc.items():
             traffic.setdefault(str(grid), {})[counter] = sum(v) / len(v)
-    if a.sq:
+    for sq_dir in a.sq:
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
-        for r in rows(a.sq, "counter_collection"):
+        for r in rows(sq_dir, "counter_collection"):
             if a.kernel in r["Kernel_Name"]:
                 px = int(r["Grid_Size"]) * pixels_per_thread(r["Kernel_Name"])
                 acc[px][r["Counter_Name"]].append(float(r["Counter_Value"]))
