@@ -222,20 +222,11 @@ __device__ __forceinline__ void pass_body(bool pass, float ss, float r, int k, f
   // Scalar branch around the sqrt: most culled spheres pass for no lane of
   // the wave in a given step, and then the whole body is skipped (the
   // compiler would otherwise if-convert it and run the sqrt every time).
-  const uint64_t pm = __builtin_amdgcn_ballot_w64(pass);
-  if (pm) {
+  // sqrt_cr_normal also serves ss < 2^-96: see pass_body_r (NOTINY).
+  if (__builtin_amdgcn_ballot_w64(pass)) {
     __asm__ volatile("; sphere passes for some lane");  // keeps the branch (no if-conversion)
-    // Uniform choice of the sqrt sequence: ballots of plain compares combined
-    // in SALU (a ballot of `pass && tiny`, or a bool select, is rematerialised
-    // through VGPRs on every visit).
-    if ((__builtin_amdgcn_ballot_w64(ss < kTinySqrtArg) & pm) == 0) {
-      if (pass) {
-        const float t = r - sqrt_cr_normal(ss);
-        L = max_nonneg(L, t);
-        dnew = k;
-      }
-    } else if (pass) {
-      const float t = r - __builtin_sqrtf(ss);
+    if (pass) {
+      const float t = r - sqrt_cr_normal(ss);
       L = max_nonneg(L, t);
       dnew = k;
     }
@@ -577,7 +568,11 @@ __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int t
 // Pass bodies of one sphere for the lane's R rays under one scalar branch.
 // (Lane-masked selects through inline asm instead of these exec-masked
 // updates were measured slower: 1% at R = 2, 15% at R = 1.)
-template <int R>
+// NOTINY: sqrt_cr_normal for every passing lane.  Exact also for ss < 2^-96,
+// where sqrt_cr_normal is not the correctly rounded sqrt: a pass needs
+// rad - sqrtf(ss) > 0.01f, so rad > 2^-7, and rad - q == rad for any q < 2^-33,
+// which both roots of such ss are (tests/native/wave_check.hip, every ss).
+template <int R, bool NOTINY = false>
 __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, float rad, int k,
                                             float (&L)[R], int (&dnew)[R]) {
   uint64_t pm[R], any = 0;
@@ -585,6 +580,20 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
   for (int r = 0; r < R; r++) {
     pm[r] = __builtin_amdgcn_ballot_w64(ss[r] < s_pass);
     any |= pm[r];
+  }
+  if (NOTINY) {
+    if (any) {
+      __asm__ volatile("; sphere passes for some ray of the wave");
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (ss[r] < s_pass) {
+          const float t = rad - sqrt_cr_normal(ss[r]);
+          L[r] = max_nonneg(L[r], t);
+          dnew[r] = k;
+        }
+      }
+    }
+    return;
   }
   if (any) {
     __asm__ volatile("; sphere passes for some ray of the wave");
@@ -620,7 +629,13 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
 // kFlPair -- visits taken two at a time: both records loaded, both spheres'
 // distances computed (four independent chains per lane), then the two pass
 // bodies in index order.
-constexpr int kFlMask = 1, kFlFree = 2, kFlPrefetch = 4, kFlPair = 8;
+// kFlNoShade (timing probe only, wrong bytes): store a hash of the march result
+// instead of shading it, to split the kernel time between march and shading.
+// kFlNoTiny -- no tiny-argument sqrt branch in the pass body (pass_body_r).
+// kFlBits -- the visit loop clears each visited bit with s_bitset0_b64.
+constexpr int kFlMask = 1, kFlFree = 2, kFlPrefetch = 4, kFlPair = 8, kFlNoShade = 32,
+              kFlNoTiny = 64, kFlBits = 128;
+constexpr int kFlDefault = kFlMask | kFlFree | kFlNoTiny;
 
 template <int SLOTS, int R, int WPB, int TLO_EVERY = 1, int FL = 0>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
@@ -698,7 +713,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     float ss[R];
 #pragma unroll
     for (int r = 0; r < R; r++) ss[r] = dist2(px[r], py[r], pz[r], cx, cy, cz);
-    pass_body_r<R>(ss, s_pass, rad, k, L, dnew);
+    pass_body_r<R, (FL & kFlNoTiny) != 0>(ss, s_pass, rad, k, L, dnew);
   };
   int trips = 1;
   if (SLOTS > 0 && windowed && __builtin_popcountll(m) <= SLOTS) {
@@ -807,6 +822,13 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
             k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
           }
         }
+      } else if (FL & kFlBits) {
+        for (uint64_t mm = win; mm;) {
+          const int k = __builtin_ctzll(mm);
+          __asm__("s_bitset0_b64 %0, %1" : "+s"(mm) : "s"(k));
+          const SphereRec& s = sph[k];
+          visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+        }
       } else {
         for (uint64_t mm = win; mm; mm &= mm - 1) {
           const int k = __builtin_ctzll(mm);
@@ -821,6 +843,11 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (valid[r]) {
+      if (FL & kFlNoShade) {
+        f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] =
+            __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^ __float_as_uint(pz[r]) ^ (uint32_t)draw[r];
+        continue;
+      }
       const SphereRec d = sph[draw[r]];
       const uint32_t rgba = shade(f, d, px[r], py[r], pz[r], nullptr);
       f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] = rgba;
@@ -1011,13 +1038,14 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
                    : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
                    : f.variant == 72 ? 3
                    : f.variant == 73 ? 4
-                   : f.variant == 74 || f.variant == 75 ? 1
-                   : f.variant >= 60 && f.variant <= 71 ? 2
+                   : f.variant == 74 || f.variant == 75 || f.variant == 83 || f.variant == 91 ? 1
+                   : (f.variant >= 60 && f.variant <= 71) || (f.variant >= 80 && f.variant <= 82) || f.variant == 90 ? 2
                    : f.variant == 42 ? 3
                    : f.variant == 43 ? 4
                    : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
   if (f.n <= kInlineSpheres &&
-      (rays > 1 || f.variant == 0 || f.variant == 49 || f.variant == 74 || f.variant == 75)) {
+      (rays > 1 || f.variant == 0 || f.variant == 49 || f.variant == 74 || f.variant == 75 ||
+       f.variant == 83 || f.variant == 91)) {
     // (8 rays) x 8 tiles: several pixels per lane
     InlineArgs args;
     args.f = f;
@@ -1029,9 +1057,11 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     // SFRT_OPT_VARIANT (A/B only): 40 / 41: four waves per workgroup, low end every
     // step, 4 / 0 slots; 42 / 43: 24x8 / 32x8 tiles; 44 / 45: one / two waves per
     // workgroup, low end every step; 48: low end every 4th step; 49: 8x8 tiles here;
-    // 47: the default without FL flags; 61-71: 60 + FL bits (kFlMask 1, kFlFree 2,
-    // kFlPrefetch 4, kFlPair 8); 72 / 73 / 74: 24x8 / 32x8 / 8x8 tiles with the
-    // default flags, 75: 8x8 with kFlPair.  Measured: DESIGN.md 5.
+    // 47: no FL flags; 61-71: 60 + FL bits (kFlMask 1, kFlFree 2, kFlPrefetch 4,
+    // kFlPair 8); 72 / 73 / 74: 24x8 / 32x8 / 8x8 tiles with FL 3, 75: 8x8 with
+    // kFlPair; 81 / 82: FL 3 | kFlBits, default | kFlBits; 80 / 83: the defaults
+    // (16x8 / 8x8, kFlDefault); 90 / 91: timing probes without shading (wrong
+    // bytes).  Measured: DESIGN.md 5.
     switch (f.variant) {
       case 40: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2>), g4, b4, 0, s, args); break;
       case 41: hipLaunchKernelGGL((k_trace_window_r<0, 2>), g4, b4, 0, s, args); break;
@@ -1055,13 +1085,21 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
         hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlMask | kFlFree>), g1, b1, 0, s, args);
         break;
       case 75: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, 11>), g1, b1, 0, s, args); break;
+      case 81: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 3 | kFlBits>), g1, b1, 0, s, args); break;
+      case 82:
+        hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 3 | kFlNoTiny | kFlBits>), g1, b1, 0, s, args);
+        break;
+      case 90: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault | kFlNoShade>), g1, b1, 0, s, args); break;
+      case 91: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlDefault | kFlNoShade>), g1, b1, 0, s, args); break;
       case 47: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2>), g1, b1, 0, s, args); break;
-      case 63:
+      case 63: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 3>), g1, b1, 0, s, args); break;
+      case 80:
+      case 83:
       default:
-        if (rays == 1)  // default for n <= kPairMinSpheres: 8x8 tiles (= variant 74)
-          hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlMask | kFlFree>), g1, b1, 0, s, args);
-        else
-          hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlMask | kFlFree>), g1, b1, 0, s, args);
+        if (rays == 1)  // default for n <= kPairMinSpheres: 8x8 tiles (= variant 83)
+          hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlDefault>), g1, b1, 0, s, args);
+        else  // (= variant 80)
+          hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault>), g1, b1, 0, s, args);
         break;
     }
   } else if (f.n <= kInlineSpheres) {

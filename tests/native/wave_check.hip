@@ -45,6 +45,26 @@ __global__ void k_check(int rounds, unsigned long long* bad) {
   if (nbad) atomicAdd(bad, nbad);
 }
 
+// The march's pass body takes sqrt_cr_normal for every passing lane, also when
+// the squared distance is below 2^-96 where sqrt_cr_normal is not the correctly
+// rounded sqrt.  A pass needs rad - sqrtf(ss) > 0.01f, so rad > 0.01f; then
+// rad - q == rad for any q < 2^-33, which both square roots of such ss are.
+// Checked here for every binary32 ss in [0, 2^-96) and radii from 0.01f up.
+__global__ void k_sqrt_tiny(unsigned long long* bad) {
+  const float rads[] = {0.01f, 0.0100001f, 0.015625f, 0.0156250019f, 0.5f, 1.0f, 2.0f,
+                        3.99999976f, 4.0f, 7.0f, 1.0e6f, 3.0e38f};
+  unsigned long long nbad = 0;
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < 0x0F800000u;
+       u += gridDim.x * blockDim.x) {
+    const float x = __uint_as_float(u);
+    const float q = sfrt::sqrt_cr_normal(x), ref = __builtin_sqrtf(x);
+    if (!(q < 0x1.0p-40f)) nbad++;
+    for (float rad : rads)
+      if (__float_as_uint(rad - q) != __float_as_uint(rad - ref)) nbad++;
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
 int main() {
   unsigned long long* d_bad = nullptr;
   if (hipMalloc(&d_bad, sizeof(*d_bad)) != hipSuccess) return 2;
@@ -52,6 +72,11 @@ int main() {
   hipLaunchKernelGGL(k_check, dim3(4096), dim3(256), 0, 0, 64, d_bad);
   unsigned long long bad = 0;
   if (hipMemcpy(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+  hipLaunchKernelGGL(k_sqrt_tiny, dim3(8192), dim3(256), 0, 0, d_bad);
+  unsigned long long bad_all = 0;
+  if (hipMemcpy(&bad_all, d_bad, sizeof(bad_all), hipMemcpyDeviceToHost) != hipSuccess) return 2;
+  std::printf("sqrt_tiny: %llu mismatches over [0, 2^-96)\n", bad_all - bad);
+  bad = bad_all;
   std::printf("waves=%d mismatches=%llu\n", 4096 * 4 * 64, bad);
   (void)hipFree(d_bad);
   return bad ? 1 : 0;

@@ -96,7 +96,7 @@ def test_cull_on_off_identical(world, floor):
 
 
 @pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 35, 36, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 52,
-                                     61, 62, 63, 64, 67, 71, 72, 73, 74, 75])
+                                     61, 62, 63, 64, 67, 71, 72, 73, 74, 75, 80, 81, 82, 83])
 def test_kernel_variants_identical(world, floor, variant):
     """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
     produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
@@ -286,7 +286,8 @@ def test_device_div_recip(tmp_path):
 
 
 def test_wave_helpers(tmp_path):
-    """wave_min_u32 / wave_max_u32 / uniform_u64 (sfrt_device.h) against a lane loop."""
+    """wave_min_u32 / wave_max_u32 / uniform_u64 (sfrt_device.h) against a lane loop, and
+    sqrt_cr_normal in the march pass body for squared distances below 2^-96."""
     exe = tmp_path / "wave_check"
     src = os.path.join(ROOT, "tests", "native", "wave_check.hip")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
