@@ -62,16 +62,21 @@ def measured_traffic(pixels: int):
         doc = json.load(open(path))
         if doc.get("kernel", "k_trace") != "k_trace":
             continue
-        ent = doc.get("per_launch_pixels", doc.get("per_grid_threads", {})).get(str(pixels))
-        if ent:
-            return ent, os.path.relpath(path, ROOT)
+        table = doc.get("per_launch_pixels", doc.get("per_grid_threads", {}))
+        for extra in (0, 64, 128):  # + the tile-order sorter workgroup (64 x R pixels)
+            ent = table.get(str(pixels + extra))
+            if ent:
+                return ent, os.path.relpath(path, ROOT)
     return None, None
 
 
-def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream):
+def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream, per_frame=None):
     """Warmup, then `steps` timed frames through the pipeline.  Returns (wall seconds,
-    kernel ms per frame from HIP events around each render on the launch stream)."""
+    kernel ms per frame from HIP events around each render on the launch stream).
+    per_frame(k), if given, runs before frame k is queued (a moving camera)."""
     for k in range(warmup):
+        if per_frame:
+            per_frame(k)
         world.render_band(pipe.acquire(k).data_ptr(), pitch, pipe.row0, pipe.rows,
                           stream.cuda_stream)
         pipe.submit(k)
@@ -84,6 +89,8 @@ def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
+        if per_frame:
+            per_frame(warmup + k)
         band = pipe.acquire(k)
         starts[k].record(stream)
         world.render_band(band.data_ptr(), pitch, pipe.row0, pipe.rows, stream.cuda_stream)
@@ -308,6 +315,27 @@ def main() -> None:
             "fps": round(args.steps / wall3, 2), "kernel_ms": round(k3, 4)}
         w3.close()
         del pipe3
+        # The adaptive tile order dispatches each frame's tiles longest-first
+        # by the march steps two frames back.  The same workload with a camera turning every
+        # frame (the order always two poses stale), and in plain row-major order.
+        pipe4 = BandPipeline(0, 1, height, pitch, "cuda")
+
+        def turn(k):
+            w.set_scene(scene.posed(0.004 * k, 0.0), WIDTH, height)
+        wall4, k4 = time_frames(w, pipe4, pitch, args.steps, args.warmup, stream, per_frame=turn)
+        result["also"]["3840x2160_lcg64_turning"] = {
+            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall4 / 1e6, 2),
+            "fps": round(args.steps / wall4, 2), "kernel_ms": round(k4, 4),
+            "camera": "rotation += 0.004 rad per frame from 0"}
+        w.set_scene(scene, WIDTH, height)
+        w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+        wall5, k5 = time_frames(w, pipe4, pitch, args.steps, args.warmup, stream)
+        w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+        result["also"]["3840x2160_lcg64_row_major"] = {
+            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall5 / 1e6, 2),
+            "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4),
+            "tile_order": "row-major (SFRT_OPT_TILE_ORDER 0)"}
+        del pipe4
         if not args.no_cpu_baseline:
             torch.cuda.synchronize()
             gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()

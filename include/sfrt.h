@@ -138,9 +138,14 @@ SFRT_API int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count
 /* Options: SFRT_OPT_CULL (1 = per-wave sphere culling, default; 0 = visit
  * every sphere -- same bytes, slower; used by A/B parity tests).
  * SFRT_OPT_VARIANT: kernel tuning variant for A/B timing (0 = default build;
- * every variant produces the same bytes). */
+ * every variant produces the same bytes).
+ * SFRT_OPT_TILE_ORDER (1 = default): sfrt_world_render_band dispatches the tiles
+ * of a frame longest-first by the march steps an earlier render_band of the same
+ * geometry recorded (two frames back; the sort runs on a world-owned stream,
+ * overlapped); 0 = row-major order.  Scheduling only: same bytes either way. */
 #define SFRT_OPT_CULL 1
 #define SFRT_OPT_VARIANT 2
+#define SFRT_OPT_TILE_ORDER 3
 SFRT_API int sfrt_world_set_option(sfrt_world* w, int option, int value);
 
 /* ---- stateless helpers ---- */

@@ -55,6 +55,18 @@ struct FrameRec {
   const uint32_t* tex;              // RGBA8 texture atlas (every loaded slot, back to back)
   const SphereRec* spheres;         // device copy (used when n > kInlineSpheres)
   int* status;                      // device word: bit 0 = march guard hit, bit 1 = bad texel
+  // Adaptive tile order ("Tile order"), one-wave-per-workgroup
+  // kernels only; all null = row-major order, nothing recorded.  Launch k of a
+  // chain (stream-ordered launches with one tile grid) dispatches tile slot s on
+  // tile tile_order[s] (longest tiles of launch k-2 first) and records each
+  // tile's march-step bucket (tile_bucket) in tile_cost.  With prev_cost set the
+  // grid has one extra workgroup, 0, dispatched first: it sorts launch k-1's
+  // buckets into next_order for launch k+1 (counting sort in its LDS, no global
+  // atomics) and renders nothing; tile slot s is then workgroup s + 1.
+  const uint32_t* tile_order;
+  uint8_t* tile_cost;
+  const uint8_t* prev_cost;
+  uint32_t* next_order;
 };
 
 // Kernel argument for n <= kInlineSpheres: frame + spheres in the kernarg segment.
@@ -74,6 +86,10 @@ struct PixelDump {
 
 // sphere_trace.hip
 int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream);
+// Tile grid of the kernel launch_trace picks for f when that kernel takes part in
+// the adaptive tile order: a key naming the grid (> 0) and its tile count; else 0.
+long long trace_tile_key(const FrameRec& f, long long* tiles);
+constexpr int kTileBuckets = 256;  // march-step buckets of the tile order (steps >= 255 share one)
 int launch_trace_points(const FrameRec& f, const int* dev_ij, int count, PixelDump* dev_out,
                         void* stream);
 

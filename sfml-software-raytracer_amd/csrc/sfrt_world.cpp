@@ -136,11 +136,28 @@ struct sfrt_world {
   uint32_t tex_off[SFRT_TEXTURE_SLOTS] = {};  // texel offset of each slot in the atlas
   int cull = 1;
   int variant = 0;
+  int tile_order_on = 1;  // SFRT_OPT_TILE_ORDER
   // --- device resources ---
   hipStream_t stream = nullptr;
   uint32_t* d_tex = nullptr;  // texture atlas: every loaded slot, back to back
   size_t d_tex_texels = 0;
   int* d_status = nullptr;
+  // Adaptive tile order for render_band ("Tile order"; FrameRec in
+  // sfrt_trace.h).  Launch k of the chain reads order[k % 2], records into
+  // cost[k % 2] and sorts cost[(k+1) % 2] (launch k-1's) into order[(k+1) % 2];
+  // consecutive launches run in stream order (a launch on another stream first
+  // waits for the previous one).
+  struct TileSched {
+    uint32_t* order[2] = {};
+    uint8_t* cost[2] = {};
+    long long cap = 0;
+    int64_t k = 0;
+    long long key_prev = 0;        // tile grid of launch k-1 (0: none)
+    bool sorted_prev = false;      // launch k-1 sorted launch k-2's tiles into order[k % 2]
+    hipStream_t last_stream = nullptr;
+    hipEvent_t last_ev = nullptr;
+    bool have_last = false;
+  } sched;
   // Device copies of the sphere records for launches that read them from memory
   // (> 64 spheres, trace_points): a ring of slots, each with pinned staging and
   // the event of the last launch that read it, so a slot is never overwritten
@@ -184,6 +201,11 @@ struct sfrt_world {
       if (p.copied) (void)hipEventDestroy(p.copied);
     }
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    for (int k = 0; k < 2; k++) {
+      (void)hipFree(sched.order[k]);
+      (void)hipFree(sched.cost[k]);
+    }
+    if (sched.last_ev) (void)hipEventDestroy(sched.last_ev);
     (void)hipFree(d_tex);
     (void)hipFree(d_status);
     (void)hipDeviceSynchronize();
@@ -331,6 +353,59 @@ struct sfrt_world {
     HIP_TRY(hipEventRecord(spheres_ev[staged], s));
     spheres_pending[staged] = true;
     staged = -1;
+    return SFRT_OK;
+  }
+
+  // Before a render_band launch on s: link f into the tile-order chain.
+  int sched_begin(sfrt::FrameRec& f, hipStream_t s) {
+    long long tiles = 0;
+    const long long key = tile_order_on ? sfrt::trace_tile_key(f, &tiles) : 0;
+    if (key == 0) return SFRT_OK;  // this launch takes no part (the chain is left as it is)
+    if (tiles > sched.cap) {       // (re)allocate; a new chain starts
+      HIP_TRY(hipDeviceSynchronize());
+      for (int k = 0; k < 2; k++) {
+        (void)hipFree(sched.order[k]);
+        (void)hipFree(sched.cost[k]);
+        sched.order[k] = nullptr;
+        sched.cost[k] = nullptr;
+      }
+      sched.cap = 0;
+      for (int k = 0; k < 2; k++) {
+        HIP_TRY(hipMalloc(&sched.order[k], sizeof(uint32_t) * (size_t)tiles));
+        HIP_TRY(hipMalloc(&sched.cost[k], (size_t)tiles));
+      }
+      if (!sched.last_ev) HIP_TRY(hipEventCreateWithFlags(&sched.last_ev, hipEventDisableTiming));
+      sched.cap = tiles;
+      sched.k = 0;
+      sched.key_prev = 0;
+      sched.sorted_prev = false;
+      sched.have_last = false;
+    }
+    if (sched.have_last && sched.last_stream != s) HIP_TRY(hipStreamWaitEvent(s, sched.last_ev, 0));
+    const int64_t k = sched.k;
+    const bool same = sched.key_prev == key;  // launch k-1 had this tile grid
+    f.tile_order = (same && sched.sorted_prev) ? sched.order[k & 1] : nullptr;
+    f.tile_cost = sched.cost[k & 1];
+    f.prev_cost = same ? sched.cost[(k + 1) & 1] : nullptr;
+    f.next_order = sched.order[(k + 1) & 1];
+    if (tile_order_on == 2 && sched.sorted_prev && same) {
+      // timing probe only: keep dispatching the last order built (by launch k-1), no
+      // sorter, the chain does not advance
+      f.prev_cost = nullptr;
+      return SFRT_OK;
+    }
+    sched.sorted_prev = same;
+    sched.key_prev = key;
+    sched.k = k + 1;
+    return SFRT_OK;
+  }
+
+  // After a launch that took part in the chain.
+  int sched_end(const sfrt::FrameRec& f, hipStream_t s) {
+    if (!f.tile_cost) return SFRT_OK;
+    HIP_TRY(hipEventRecord(sched.last_ev, s));
+    sched.last_stream = s;
+    sched.have_last = true;
     return SFRT_OK;
   }
 
@@ -518,6 +593,10 @@ int sfrt_world_set_option(sfrt_world* w, int option, int value) {
     w->variant = value;
     return SFRT_OK;
   }
+  if (option == SFRT_OPT_TILE_ORDER) {
+    w->tile_order_on = value == 2 ? 2 : value ? 1 : 0;  // 2: timing probe (see sched_begin)
+    return SFRT_OK;
+  }
   return SFRT_E_INVALID;
 }
 
@@ -600,7 +679,9 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   f.out_pitch = pitch_bytes / 4;
   rc = w->stage_spheres(f, recs, s, false);
   if (rc) return rc;
+  if ((rc = w->sched_begin(f, s))) return rc;
   if (sfrt::launch_trace(f, recs.data(), s)) return SFRT_E_HIP;
+  if ((rc = w->sched_end(f, s))) return rc;
   return w->launched(s);
 }
 
@@ -700,7 +781,9 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
   f.status = slot.d_status;
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
+  if ((rc = w->sched_begin(f, w->stream))) return rc;  // adaptive tile order, as render_band
   if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
+  if ((rc = w->sched_end(f, w->stream))) return rc;
   if ((rc = w->launched(w->stream))) return rc;
   HIP_TRY(hipEventRecord(slot.rendered, w->stream));
   HIP_TRY(hipStreamWaitEvent(w->copy_stream, slot.rendered, 0));

@@ -637,12 +637,87 @@ constexpr int kFlMask = 1, kFlFree = 2, kFlPrefetch = 4, kFlPair = 8, kFlNoShade
               kFlNoTiny = 64, kFlBits = 128;
 constexpr int kFlDefault = kFlMask | kFlFree | kFlNoTiny;
 
+// Tile-order bucket of a tile's march steps: longest first.
+__device__ __forceinline__ uint32_t tile_bucket(uint32_t steps) {
+  constexpr uint32_t top = (uint32_t)kTileBuckets - 1u;
+  return top - (steps < top ? steps : top);
+}
+
+// Counting sort of n tiles by their step buckets, longest first, by one wave
+// with a 256-entry histogram in LDS: count, exclusive scan, then rank each tile
+// with a returning LDS atomic and store order[rank] = tile.  Each lane owns one
+// contiguous chunk of tiles read 16 buckets per 16-byte load, eight loads in
+// flight at a time (the passes are bound by load latency); the lanes of one
+// atomic then touch tiles far apart in the frame, whose buckets differ (same-
+// address LDS atomics serialise).  Order within a bucket is unspecified.
+__device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int n,
+                                           uint32_t* __restrict__ order) {
+  __shared__ uint32_t cnt[kTileBuckets];
+  const int lane = threadIdx.x & 63;
+  for (int q = lane; q < kTileBuckets; q += 64) cnt[q] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  const int nvec = n >> 4;
+  const int per = (nvec + 63) >> 6;  // 16-byte vectors per lane
+  const int v0 = lane * per < nvec ? lane * per : nvec;
+  const int v1 = v0 + per < nvec ? v0 + per : nvec;
+  const uint4* __restrict__ cv = reinterpret_cast<const uint4*>(cost);
+  auto pass = [&](auto&& one) {
+    for (int v = v0; v < v1; v += 8) {
+      uint4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) q[u] = v + u < v1 ? cv[v + u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (v + u >= v1) break;
+        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+        for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
+      }
+    }
+    for (int t = nvec * 16 + lane; t < n; t += 64) one((uint32_t)cost[t], t);
+  };
+  pass([&](uint32_t b, int) { atomicAdd(&cnt[b], 1u); });
+  __builtin_amdgcn_wave_barrier();
+  {  // exclusive scan, 4 buckets per lane
+    const uint32_t a = cnt[4 * lane], b = cnt[4 * lane + 1], c = cnt[4 * lane + 2],
+                   d = cnt[4 * lane + 3];
+    const uint32_t sum = (a + b) + (c + d);
+    uint32_t incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t up = (uint32_t)__shfl_up((int)incl, off, 64);
+      if (lane >= off) incl += up;
+    }
+    const uint32_t base = incl - sum;
+    cnt[4 * lane] = base;
+    cnt[4 * lane + 1] = base + a;
+    cnt[4 * lane + 2] = base + a + b;
+    cnt[4 * lane + 3] = base + a + b + c;
+  }
+  __builtin_amdgcn_wave_barrier();
+  pass([&](uint32_t b, int t) { order[atomicAdd(&cnt[b], 1u)] = (uint32_t)t; });
+}
+
 template <int SLOTS, int R, int WPB, int TLO_EVERY = 1, int FL = 0>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
                                                     const SphereRec* __restrict__ sph) {
   const int lane = threadIdx.x & 63;
   const int wave = WPB == 1 ? 0 : (int)(threadIdx.x >> 6);
-  const int tile = blockIdx.x * WPB + wave;
+  // Adaptive tile order (sfrt_trace.h FrameRec): workgroup 0 may be the sorter.
+  const int ntiles = f.tiles_x * ((f.sub_rows + kTile - 1) / kTile);
+  int slot = (int)blockIdx.x;
+  if (WPB == 1 && f.prev_cost) {
+    if (blockIdx.x == 0) {
+      sort_tiles(f.prev_cost, ntiles, f.next_order);
+      return;
+    }
+    slot -= 1;
+  }
+  int tile = slot * WPB + wave;
+  if (WPB == 1 && f.tile_order) {
+    const int t = (int)f.tile_order[slot];
+    tile = t < ntiles ? t : slot;  // never outside the grid
+  }
   const int tile_y = tile / f.tiles_x;  // f.tiles_x = ceil(sub_w / (8 R)) for this kernel
   const int tile_x = tile - tile_y * f.tiles_x;
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
@@ -689,6 +764,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     const Cone cone = tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
     m = cull_window(f, sph, 0, cone, lo, hi);
   }
+
   // pos += dir * L for marching rays (SphereWorld.cpp:371).  kFlFree: on every
   // lane.  A ray that stopped had no passing sphere at its position (its last
   // step visited every sphere that could pass), its position no longer moves,
@@ -840,6 +916,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
   }
   if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
+  if (WPB == 1 && f.tile_cost && lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket((uint32_t)trips);
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (valid[r]) {
@@ -1021,6 +1098,36 @@ __global__ __launch_bounds__(256) void k_trace_points(FrameRec f, const int* __r
 
 }  // namespace
 
+// The kernel choice of launch_trace, shared with trace_tile_key.
+static int trace_rays(const FrameRec& f) {
+  return f.variant == 49 ? 1
+         : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
+         : f.variant == 72 ? 3
+         : f.variant == 73 ? 4
+         : f.variant == 74 || f.variant == 75 || f.variant == 83 || f.variant == 91 ? 1
+         : (f.variant >= 60 && f.variant <= 71) || (f.variant >= 80 && f.variant <= 82) || f.variant == 90 ? 2
+         : f.variant == 42 ? 3
+         : f.variant == 43 ? 4
+         : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
+}
+static bool trace_window_r(const FrameRec& f, int rays) {
+  return f.n <= kInlineSpheres &&
+         (rays > 1 || f.variant == 0 || f.variant == 49 || f.variant == 74 || f.variant == 75 ||
+          f.variant == 83 || f.variant == 91);
+}
+
+long long trace_tile_key(const FrameRec& f, long long* tiles) {
+  *tiles = 0;
+  const int rays = trace_rays(f);
+  // one wave per workgroup: every R-kernel launch except variants 40-43 and 45
+  if (!trace_window_r(f, rays) || (f.variant >= 40 && f.variant <= 43) || f.variant == 45) return 0;
+  const long long tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
+  const long long tiles_y = (f.sub_rows + kTile - 1) / kTile;
+  if (tiles_x <= 0 || tiles_y <= 0) return 0;
+  *tiles = tiles_x * tiles_y;
+  return (1ll << 62) | ((long long)rays << 56) | (tiles_x << 28) | tiles_y;
+}
+
 int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream) {
   const long long tiles_y = (f.sub_rows + kTile - 1) / kTile;
   const long long tiles = tiles_y * f.tiles_x;
@@ -1034,25 +1141,20 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
   // workgroup (a finished wave's slot is refilled at once), refresh the march
   // window's low end every second step and use kFlMask | kFlFree (measured,
   // DESIGN.md 5).
-  const int rays = f.variant == 49 ? 1
-                   : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
-                   : f.variant == 72 ? 3
-                   : f.variant == 73 ? 4
-                   : f.variant == 74 || f.variant == 75 || f.variant == 83 || f.variant == 91 ? 1
-                   : (f.variant >= 60 && f.variant <= 71) || (f.variant >= 80 && f.variant <= 82) || f.variant == 90 ? 2
-                   : f.variant == 42 ? 3
-                   : f.variant == 43 ? 4
-                   : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
-  if (f.n <= kInlineSpheres &&
-      (rays > 1 || f.variant == 0 || f.variant == 49 || f.variant == 74 || f.variant == 75 ||
-       f.variant == 83 || f.variant == 91)) {
+  const int rays = trace_rays(f);
+  if (trace_window_r(f, rays)) {
     // (8 rays) x 8 tiles: several pixels per lane
     InlineArgs args;
     args.f = f;
     args.f.tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
     const long long tiles2 = tiles_y * args.f.tiles_x;
-    const dim3 g1((unsigned)tiles2), b1(64);  // one wave per workgroup
+    long long key_tiles = 0;
+    if (trace_tile_key(f, &key_tiles) == 0 || key_tiles != tiles2) {  // no adaptive order here
+      args.f.tile_order = nullptr; args.f.tile_cost = nullptr; args.f.prev_cost = nullptr;
+    }
+    // one wave per workgroup (+ the tile-order sorter, sfrt_trace.h FrameRec)
+    const dim3 g1((unsigned)(tiles2 + (args.f.prev_cost ? 1 : 0))), b1(64);
     const dim3 g4((unsigned)((tiles2 + kWavesPerBlock - 1) / kWavesPerBlock)), b4(256);
     // SFRT_OPT_VARIANT (A/B only): 40 / 41: four waves per workgroup, low end every
     // step, 4 / 0 slots; 42 / 43: 24x8 / 32x8 tiles; 44 / 45: one / two waves per

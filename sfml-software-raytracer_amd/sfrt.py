@@ -20,6 +20,7 @@ LIB_PATH = os.path.join(HERE, "libsfrt.so")
 
 SFRT_OPT_CULL = 1
 SFRT_OPT_VARIANT = 2
+SFRT_OPT_TILE_ORDER = 3
 ERRORS = {
     0: "SFRT_OK", -1: "SFRT_E_INVALID", -2: "SFRT_E_EMPTY", -3: "SFRT_E_NO_TEXTURE",
     -4: "SFRT_E_TOO_MANY", -5: "SFRT_E_HIP", -6: "SFRT_E_MARCH_LIMIT", -7: "SFRT_E_TEXEL",

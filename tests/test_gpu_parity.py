@@ -405,3 +405,77 @@ def test_random_subsets_match_oracle(world, floor):
         oracle_for(sc, width, height, floor).update_image(want, ystart, yadd, xstart, xadd)
         msg = diff_report(got, want, width)
         assert not msg, f"seed {seed} subset ({ystart},{yadd},{xstart},{xadd}): {msg}"
+
+
+def test_adaptive_tile_order_same_bytes(world, floor):
+    """SFRT_OPT_TILE_ORDER (render_band dispatches tiles longest-first by the march steps of
+    two frames back): every frame of a sequence on a poisoned device buffer equals the
+    row-major frame and the oracle -- static pose (exact order from frame 2 on), a pose
+    changing every frame, scene size switches (16x8 <-> 8x8 tiles), bands and resolutions
+    changing mid-sequence (stale orders must be dropped), two streams alternating."""
+    import sfrt
+    import torch
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    seq = []
+    for k in range(5):
+        seq.append((scenes.lcg64(), (0.0, 0.0), 640, 360, 0, 360))
+    for k in range(5):
+        seq.append((scenes.lcg64(), (0.3 * k, -0.1 * k), 640, 360, 0, 360))
+    for k in range(4):
+        seq.append((scenes.default10(), (0.2 * k, 0.1), 640, 360, 0, 360))
+    seq += [(scenes.lcg64(), (1.1, -0.2), 640, 360, 40, 200), (scenes.lcg64(), (1.1, -0.2), 640, 360, 40, 200),
+            (scenes.lcg64(), (1.1, -0.2), 333, 211, 0, 211), (scenes.lcg64(), (1.1, -0.2), 640, 360, 40, 200),
+            (scenes.lcg64(), (1.1, -0.2), 640, 360, 40, 200), (scenes.lcg64(), (1.1, -0.2), 640, 360, 0, 360)]
+    ref = {}
+    try:
+        for k, (sc, pose, width, height, r0, rows) in enumerate(seq):
+            scene = sc.posed(*pose)
+            key = (sc.name, pose, width, height)
+            if key not in ref:
+                world.set_scene(scene, width, height)
+                ref[key] = oracle_for(scene, width, height, floor).render(host_threads())
+            world.set_scene(scene, width, height)
+            stream = (s1 if k % 2 == 0 else s2)
+            buf = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            torch.cuda.synchronize()
+            world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+            world.render_band(buf[r0].data_ptr(), width * 4, r0, rows, stream.cuda_stream)
+            world.check(stream.cuda_stream)
+            torch.cuda.synchronize()
+            got = buf.cpu().numpy().ravel()
+            want = np.full(width * height * 4, 0xA5, dtype=np.uint8)
+            want[r0 * width * 4:(r0 + rows) * width * 4] = ref[key][r0 * width * 4:(r0 + rows) * width * 4]
+            assert diff_report(got, want, width) == "", (k, sc.name, pose, width, height, r0, rows)
+    finally:
+        world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+
+
+def test_adaptive_tile_order_4k_frames(world, floor):
+    """Twelve back-to-back 4K frames on one stream without host syncs in between (the
+    bench's pattern: the order sort overlaps the next frame), poses cycling through three
+    values: each frame equals the same pose's row-major frame."""
+    import sfrt
+    import torch
+    width, height = 3840, 2160
+    poses = [(0.0, 0.0), (1.1, -0.2), (2.5, 0.3)]
+    stream = torch.cuda.Stream()
+    rowmajor = {}
+    frames = []
+    with torch.cuda.stream(stream):  # buffers filled on the render stream
+        world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+        for p in poses:
+            world.set_scene(scenes.lcg64().posed(*p), width, height)
+            b = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda:0")
+            world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+            rowmajor[p] = b
+        world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+        for k in range(12):
+            p = poses[(k // 2) % 3]
+            world.set_scene(scenes.lcg64().posed(*p), width, height)
+            b = torch.full((height, width * 4), 0x5A, dtype=torch.uint8, device="cuda:0")
+            world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+            frames.append((p, b))
+    world.check(stream.cuda_stream)
+    torch.cuda.synchronize()
+    for k, (p, b) in enumerate(frames):
+        assert torch.equal(b, rowmajor[p]), (k, p)

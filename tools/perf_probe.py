@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--variants", default="march,nocull,outside,outside_nc")
     ap.add_argument("--kvariants", default="0",
                     help="comma list of SFRT_OPT_VARIANT values, interleaved per round")
+    ap.add_argument("--orders", default="1",
+                    help="comma list of SFRT_OPT_TILE_ORDER values (1 adaptive, 0 row-major); "
+                         "keys get /o0 for row-major")
     args = ap.parse_args()
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -63,12 +66,16 @@ def main():
                     ("outside_nc", outside, 0))
             for var, scene, cull in (v for v in allv if v[0] in args.variants.split(",")):
                 for kv in [int(x) for x in args.kvariants.split(",")]:
-                    w.set_scene(scene, width, height)
-                    w.set_option(sfrt.SFRT_OPT_CULL, cull)
-                    w.set_option(sfrt.SFRT_OPT_VARIANT, kv)
-                    med, best = time_kernel(w, buf, width, height, args.reps, stream)
-                    out.setdefault(f"{name}/{var}/k{kv}", []).append(round(med * 1e3, 2))
+                    for order in [int(x) for x in args.orders.split(",")]:
+                        w.set_scene(scene, width, height)
+                        w.set_option(sfrt.SFRT_OPT_CULL, cull)
+                        w.set_option(sfrt.SFRT_OPT_VARIANT, kv)
+                        w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+                        med, best = time_kernel(w, buf, width, height, args.reps, stream)
+                        tag = "" if order else "/o0"
+                        out.setdefault(f"{name}/{var}/k{kv}{tag}", []).append(round(med * 1e3, 2))
     w.set_option(sfrt.SFRT_OPT_CULL, 1)
+    w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
     for k, v in out.items():
         print(f"{k:32s} us(median per round) {v}")
     print(json.dumps(out))
