@@ -63,7 +63,8 @@ def measured_traffic(pixels: int):
         if doc.get("kernel", "k_trace") != "k_trace":
             continue
         table = doc.get("per_launch_pixels", doc.get("per_grid_threads", {}))
-        for extra in (0, 64, 128):  # + the tile-order sorter workgroup (64 x R pixels)
+        # the steady-state launch has the tile-order sorter workgroup (+64 x R pixels)
+        for extra in (128, 64, 0):
             ent = table.get(str(pixels + extra))
             if ent:
                 return ent, os.path.relpath(path, ROOT)
