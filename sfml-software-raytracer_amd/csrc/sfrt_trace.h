@@ -59,9 +59,9 @@ struct FrameRec {
   // kernels only; all null = row-major order, nothing recorded.  Launch k of a
   // chain (stream-ordered launches with one tile grid) dispatches tile slot s on
   // tile tile_order[s] (longest tiles of launch k-2 first) and records each
-  // tile's march-step bucket (tile_bucket) in tile_cost.  With prev_cost set the
+  // tile's march-step class (tile_bucket) in tile_cost.  With prev_cost set the
   // grid has one extra workgroup, 0, dispatched first: it sorts launch k-1's
-  // buckets into next_order for launch k+1 (counting sort in its LDS, no global
+  // classes into next_order for launch k+1 (stable counting sort in its LDS, no
   // atomics) and renders nothing; tile slot s is then workgroup s + 1.
   const uint32_t* tile_order;
   uint8_t* tile_cost;
@@ -89,7 +89,7 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
 // Tile grid of the kernel launch_trace picks for f when that kernel takes part in
 // the adaptive tile order: a key naming the grid (> 0) and its tile count; else 0.
 long long trace_tile_key(const FrameRec& f, long long* tiles);
-constexpr int kTileBuckets = 256;  // march-step buckets of the tile order (steps >= 255 share one)
+constexpr int kTileBuckets = 16;  // march-step classes of the tile order (sphere_trace.hip tile_bucket)
 int launch_trace_points(const FrameRec& f, const int* dev_ij, int count, PixelDump* dev_out,
                         void* stream);
 

@@ -637,29 +637,35 @@ constexpr int kFlMask = 1, kFlFree = 2, kFlPrefetch = 4, kFlPair = 8, kFlNoShade
               kFlNoTiny = 64, kFlBits = 128;
 constexpr int kFlDefault = kFlMask | kFlFree | kFlNoTiny;
 
-// Tile-order bucket of a tile's march steps: longest first.
+// Tile-order bucket of a tile's march steps, longest first: 16 classes, finer
+// where most tiles are (steps 4..16 at 4K).
 __device__ __forceinline__ uint32_t tile_bucket(uint32_t steps) {
-  constexpr uint32_t top = (uint32_t)kTileBuckets - 1u;
-  return top - (steps < top ? steps : top);
+  const uint32_t c = steps < 16u ? (steps < 4u ? 0u : (steps - 2u) >> 1)  // 0..6
+                     : steps < 32u ? 7u + ((steps - 16u) >> 2)             // 7..10
+                     : steps < 40u ? 11u : steps < 48u ? 12u : steps < 64u ? 13u
+                     : steps < 96u ? 14u : 15u;
+  return (uint32_t)(kTileBuckets - 1) - c;
 }
 
-// Counting sort of n tiles by their step buckets, longest first, by one wave
-// with a 256-entry histogram in LDS: count, exclusive scan, then rank each tile
-// with a returning LDS atomic and store order[rank] = tile.  Each lane owns one
-// contiguous chunk of tiles read 16 buckets per 16-byte load, eight loads in
-// flight at a time (the passes are bound by load latency); the lanes of one
-// atomic then touch tiles far apart in the frame, whose buckets differ (same-
-// address LDS atomics serialise).  Order within a bucket is unspecified.
+// Stable counting sort of n tiles by bucket (longest first; ties in tile
+// order), by one wave.  Each lane owns one contiguous chunk of tiles, read 16
+// buckets per 16-byte load with eight loads in flight (the passes are bound by
+// load latency), and its own column of a [bucket][lane] histogram in LDS, so
+// counting and ranking need no atomics; the exclusive scan runs bucket-major
+// over (bucket, lane), which keeps chunk order -- tile order -- within a bucket.
+// (Per-lane counters: LDS atomics without conflicts.)
 __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int n,
                                            uint32_t* __restrict__ order) {
-  __shared__ uint32_t cnt[kTileBuckets];
+  __shared__ uint32_t cnt[kTileBuckets][64];
   const int lane = threadIdx.x & 63;
-  for (int q = lane; q < kTileBuckets; q += 64) cnt[q] = 0u;
-  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int b = 0; b < kTileBuckets; b++) cnt[b][lane] = 0u;
   const int nvec = n >> 4;
   const int per = (nvec + 63) >> 6;  // 16-byte vectors per lane
   const int v0 = lane * per < nvec ? lane * per : nvec;
   const int v1 = v0 + per < nvec ? v0 + per : nvec;
+  // the n % 16 tail tiles go to the last lane's chunk end (after vector nvec - 1)
+  const bool tail = lane == 63;
   const uint4* __restrict__ cv = reinterpret_cast<const uint4*>(cost);
   auto pass = [&](auto&& one) {
     for (int v = v0; v < v1; v += 8) {
@@ -674,28 +680,26 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
         for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
       }
     }
-    for (int t = nvec * 16 + lane; t < n; t += 64) one((uint32_t)cost[t], t);
+    if (tail)
+      for (int t = nvec * 16; t < n; t++) one((uint32_t)cost[t], t);
   };
-  pass([&](uint32_t b, int) { atomicAdd(&cnt[b], 1u); });
-  __builtin_amdgcn_wave_barrier();
-  {  // exclusive scan, 4 buckets per lane
-    const uint32_t a = cnt[4 * lane], b = cnt[4 * lane + 1], c = cnt[4 * lane + 2],
-                   d = cnt[4 * lane + 3];
-    const uint32_t sum = (a + b) + (c + d);
-    uint32_t incl = sum;
+  // LDS atomics on the lane's own counters: no conflicts, and the count pass's
+  // need no return (a plain read-modify-write would wait on every read)
+  pass([&](uint32_t b, int) { atomicAdd(&cnt[b][lane], 1u); });
+  uint32_t run = 0;  // exclusive scan over (bucket, lane), bucket-major
+#pragma unroll
+  for (int b = 0; b < kTileBuckets; b++) {
+    const uint32_t c = cnt[b][lane];
+    uint32_t incl = c;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t up = (uint32_t)__shfl_up((int)incl, off, 64);
       if (lane >= off) incl += up;
     }
-    const uint32_t base = incl - sum;
-    cnt[4 * lane] = base;
-    cnt[4 * lane + 1] = base + a;
-    cnt[4 * lane + 2] = base + a + b;
-    cnt[4 * lane + 3] = base + a + b + c;
+    cnt[b][lane] = run + incl - c;
+    run += (uint32_t)__shfl((int)incl, 63, 64);
   }
-  __builtin_amdgcn_wave_barrier();
-  pass([&](uint32_t b, int t) { order[atomicAdd(&cnt[b], 1u)] = (uint32_t)t; });
+  pass([&](uint32_t b, int t) { order[atomicAdd(&cnt[b][lane], 1u)] = (uint32_t)t; });
 }
 
 template <int SLOTS, int R, int WPB, int TLO_EVERY = 1, int FL = 0>
