@@ -148,6 +148,74 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
   return u2f(f2u(r) ^ (hy & 0x80000000u));
 }
 
+// ---- adaptive tile order (DESIGN.md 5 "Tile order"; host side sfrt_sched.h) ----
+constexpr int kTileBuckets = 16;  // march-step classes
+
+// Tile-order bucket of a tile's march steps, longest first: 16 classes, finer
+// where most tiles are (steps 4..16 at 4K).
+__device__ __forceinline__ uint32_t tile_bucket(uint32_t steps) {
+  const uint32_t c = steps < 16u ? (steps < 4u ? 0u : (steps - 2u) >> 1)  // 0..6
+                     : steps < 32u ? 7u + ((steps - 16u) >> 2)             // 7..10
+                     : steps < 40u ? 11u : steps < 48u ? 12u : steps < 64u ? 13u
+                     : steps < 96u ? 14u : 15u;
+  return (uint32_t)(kTileBuckets - 1) - c;
+}
+
+// Stable counting sort of n tiles by bucket (longest first; ties in tile
+// order), by one wave.  Each lane owns one contiguous chunk of tiles, read 16
+// buckets per 16-byte load with eight loads in flight (the passes are bound by
+// load latency), and its own column of a [bucket][lane] histogram in LDS, so
+// counting and ranking need no atomics; the exclusive scan runs bucket-major
+// over (bucket, lane), which keeps chunk order -- tile order -- within a bucket.
+// (Per-lane counters: LDS atomics without conflicts.)
+__device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int n,
+                                           uint32_t* __restrict__ order) {
+  __shared__ uint32_t cnt[kTileBuckets][64];
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int b = 0; b < kTileBuckets; b++) cnt[b][lane] = 0u;
+  const int nvec = n >> 4;
+  const int per = (nvec + 63) >> 6;  // 16-byte vectors per lane
+  const int v0 = lane * per < nvec ? lane * per : nvec;
+  const int v1 = v0 + per < nvec ? v0 + per : nvec;
+  // the n % 16 tail tiles go to the last lane's chunk end (after vector nvec - 1)
+  const bool tail = lane == 63;
+  const uint4* __restrict__ cv = reinterpret_cast<const uint4*>(cost);
+  auto pass = [&](auto&& one) {
+    for (int v = v0; v < v1; v += 8) {
+      uint4 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) q[u] = v + u < v1 ? cv[v + u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (v + u >= v1) break;
+        const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+        for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
+      }
+    }
+    if (tail)
+      for (int t = nvec * 16; t < n; t++) one((uint32_t)cost[t], t);
+  };
+  // LDS atomics on the lane's own counters: no conflicts, and the count pass's
+  // need no return (a plain read-modify-write would wait on every read)
+  pass([&](uint32_t b, int) { atomicAdd(&cnt[b][lane], 1u); });
+  uint32_t run = 0;  // exclusive scan over (bucket, lane), bucket-major
+#pragma unroll
+  for (int b = 0; b < kTileBuckets; b++) {
+    const uint32_t c = cnt[b][lane];
+    uint32_t incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t up = (uint32_t)__shfl_up((int)incl, off, 64);
+      if (lane >= off) incl += up;
+    }
+    cnt[b][lane] = run + incl - c;
+    run += (uint32_t)__shfl((int)incl, 63, 64);
+  }
+  pass([&](uint32_t b, int t) { order[atomicAdd(&cnt[b][lane], 1u)] = (uint32_t)t; });
+}
+
 constexpr float kTinySqrtArg = 0x1.0p-96f;
 
 // Correctly rounded sqrtf for any x: the short form unless some lane of the

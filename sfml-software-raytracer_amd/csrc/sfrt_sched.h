@@ -1,0 +1,104 @@
+// sfrt_sched.h -- host side of the adaptive tile order ("Tile order")
+// shared by the one-wave-per-tile renderers (sphere_trace.hip, voxel_trace.hip;
+// device side: sfrt_device.h sort_tiles).
+//
+// Launch k of a chain (consecutive launches of one renderer object with one tile
+// grid) reads order[k % 2] (built by launch k-1 from launch k-2's costs), records
+// its per-tile march-step classes into cost[k % 2], and -- from its extra
+// workgroup 0 -- sorts cost[(k+1) % 2] (launch k-1's) into order[(k+1) % 2].
+// Consecutive launches are ordered by their stream; a launch on another stream
+// than the previous one first waits for it.  An order is used only when the two
+// launches before had the same grid (key).  Scheduling only: every tile is
+// rendered once whatever the order.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sfrt {
+
+struct TileSchedPtrs {
+  const uint32_t* tile_order = nullptr;  // slot -> tile (nullptr: row-major)
+  uint8_t* tile_cost = nullptr;          // this launch's per-tile classes (nullptr: no chain)
+  const uint8_t* prev_cost = nullptr;    // launch k-1's, to sort (nullptr: no sorter workgroup)
+  uint32_t* next_order = nullptr;        // the sorter's output, for launch k+1
+};
+
+struct TileSched {
+  uint32_t* order[2] = {};
+  uint8_t* cost[2] = {};
+  long long cap = 0;
+  int64_t k = 0;
+  long long key_prev = 0;        // tile grid of launch k-1 (0: none)
+  bool sorted_prev = false;      // launch k-1 sorted launch k-2's tiles into order[k % 2]
+  hipStream_t last_stream = nullptr;
+  hipEvent_t last_ev = nullptr;
+  bool have_last = false;
+
+  void release() {
+    for (int q = 0; q < 2; q++) {
+      (void)hipFree(order[q]);
+      (void)hipFree(cost[q]);
+      order[q] = nullptr;
+      cost[q] = nullptr;
+    }
+    cap = 0;
+    if (last_ev) (void)hipEventDestroy(last_ev);
+    last_ev = nullptr;
+  }
+
+  // Link a launch on s with tile grid `key` (0: takes no part) of `tiles` tiles
+  // into the chain.  mode: 1 = adaptive; 2 = timing probe (reuse the last order,
+  // no sorter, the chain does not advance).
+  hipError_t begin(long long key, long long tiles, hipStream_t s, int mode, TileSchedPtrs& p) {
+    p = TileSchedPtrs{};
+    if (key == 0 || mode == 0) return hipSuccess;
+    hipError_t e;
+    if (tiles > cap) {  // (re)allocate; a new chain starts
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+      hipEvent_t ev = last_ev;
+      last_ev = nullptr;
+      release();
+      last_ev = ev;
+      for (int q = 0; q < 2; q++) {
+        if ((e = hipMalloc(&order[q], sizeof(uint32_t) * (size_t)tiles)) != hipSuccess) return e;
+        if ((e = hipMalloc(&cost[q], (size_t)tiles)) != hipSuccess) return e;
+      }
+      if (!last_ev && (e = hipEventCreateWithFlags(&last_ev, hipEventDisableTiming)) != hipSuccess)
+        return e;
+      cap = tiles;
+      k = 0;
+      key_prev = 0;
+      sorted_prev = false;
+      have_last = false;
+    }
+    if (have_last && last_stream != s && (e = hipStreamWaitEvent(s, last_ev, 0)) != hipSuccess)
+      return e;
+    const bool same = key_prev == key;  // launch k-1 had this tile grid
+    p.tile_order = (same && sorted_prev) ? order[k & 1] : nullptr;
+    p.tile_cost = cost[k & 1];
+    p.prev_cost = same ? cost[(k + 1) & 1] : nullptr;
+    p.next_order = order[(k + 1) & 1];
+    if (mode == 2 && sorted_prev && same) {
+      p.prev_cost = nullptr;
+      return hipSuccess;
+    }
+    sorted_prev = same;
+    key_prev = key;
+    k++;
+    return hipSuccess;
+  }
+
+  // After the launch that took part (p.tile_cost set) was queued on s.
+  hipError_t end(const TileSchedPtrs& p, hipStream_t s) {
+    if (!p.tile_cost) return hipSuccess;
+    const hipError_t e = hipEventRecord(last_ev, s);
+    if (e != hipSuccess) return e;
+    last_stream = s;
+    have_last = true;
+    return hipSuccess;
+  }
+};
+
+}  // namespace sfrt

@@ -89,7 +89,6 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
 // Tile grid of the kernel launch_trace picks for f when that kernel takes part in
 // the adaptive tile order: a key naming the grid (> 0) and its tile count; else 0.
 long long trace_tile_key(const FrameRec& f, long long* tiles);
-constexpr int kTileBuckets = 16;  // march-step classes of the tile order (sphere_trace.hip tile_bucket)
 int launch_trace_points(const FrameRec& f, const int* dev_ij, int count, PixelDump* dev_out,
                         void* stream);
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "sfrt.h"
+#include "sfrt_sched.h"
 #include "sfrt_math.h"
 #include "voxel_trace.h"
 
@@ -107,11 +108,16 @@ struct sfrt_voxel {
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
+  int variant = 0;           // SFRT_OPT_VARIANT (A/B: 1 = the 2-D grid kernel)
+  int tile_order_on = 0;     // SFRT_OPT_TILE_ORDER: off by default here (slower)
+  sfrt::TileSched sched;     // adaptive tile order (sfrt_sched.h), render_band
   std::mutex mu;
 
   ~sfrt_voxel() {
     DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    (void)hipDeviceSynchronize();
+    sched.release();
     for (auto& t : tex) (void)hipFree(t.d);
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
@@ -382,6 +388,7 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   sfrt::VoxFrame f;
   int rc = v->prepare(f, v->stream);
   if (rc) return rc;
+  f.variant = v->variant;
   f.xstart = xstart; f.xadd = xadd; f.ystart = ystart; f.yadd = yadd;
   f.sub_w = sub_w;
   f.sub_row0 = 0;
@@ -420,8 +427,32 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   f.sub_rows = rows;
   f.out = (uint32_t*)dev_pixels;
   f.out_pitch = pitch_bytes / 4;
+  f.variant = v->variant;
+  long long tiles = 0;
+  const long long key = v->tile_order_on ? sfrt::voxel_tile_key(f, &tiles) : 0;
+  sfrt::TileSchedPtrs p;
+  HIP_TRY(v->sched.begin(key, tiles, s, v->tile_order_on, p));
+  f.tile_order = p.tile_order;
+  f.tile_cost = p.tile_cost;
+  f.prev_cost = p.prev_cost;
+  f.next_order = p.next_order;
   if (sfrt::launch_voxel(f, s)) return SFRT_E_HIP;
+  HIP_TRY(v->sched.end(p, s));
   return v->launched(s);
+}
+
+int sfrt_voxel_set_option(sfrt_voxel* v, int option, int value) {
+  if (!v) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(v->mu);
+  if (option == SFRT_OPT_VARIANT) {
+    v->variant = value;
+    return SFRT_OK;
+  }
+  if (option == SFRT_OPT_TILE_ORDER) {
+    v->tile_order_on = value == 2 ? 2 : value ? 1 : 0;
+    return SFRT_OK;
+  }
+  return SFRT_E_INVALID;
 }
 
 int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream) {

@@ -21,6 +21,7 @@
 
 #include "sfrt.h"
 #include "sfrt_math.h"
+#include "sfrt_sched.h"
 #include "sfrt_trace.h"
 
 #pragma clang fp contract(off)
@@ -142,22 +143,7 @@ struct sfrt_world {
   uint32_t* d_tex = nullptr;  // texture atlas: every loaded slot, back to back
   size_t d_tex_texels = 0;
   int* d_status = nullptr;
-  // Adaptive tile order for render_band ("Tile order"; FrameRec in
-  // sfrt_trace.h).  Launch k of the chain reads order[k % 2], records into
-  // cost[k % 2] and sorts cost[(k+1) % 2] (launch k-1's) into order[(k+1) % 2];
-  // consecutive launches run in stream order (a launch on another stream first
-  // waits for the previous one).
-  struct TileSched {
-    uint32_t* order[2] = {};
-    uint8_t* cost[2] = {};
-    long long cap = 0;
-    int64_t k = 0;
-    long long key_prev = 0;        // tile grid of launch k-1 (0: none)
-    bool sorted_prev = false;      // launch k-1 sorted launch k-2's tiles into order[k % 2]
-    hipStream_t last_stream = nullptr;
-    hipEvent_t last_ev = nullptr;
-    bool have_last = false;
-  } sched;
+  sfrt::TileSched sched;  // adaptive tile order (sfrt_sched.h), render_band / submit_frame
   // Device copies of the sphere records for launches that read them from memory
   // (> 64 spheres, trace_points): a ring of slots, each with pinned staging and
   // the event of the last launch that read it, so a slot is never overwritten
@@ -201,11 +187,7 @@ struct sfrt_world {
       if (p.copied) (void)hipEventDestroy(p.copied);
     }
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    for (int k = 0; k < 2; k++) {
-      (void)hipFree(sched.order[k]);
-      (void)hipFree(sched.cost[k]);
-    }
-    if (sched.last_ev) (void)hipEventDestroy(sched.last_ev);
+    sched.release();
     (void)hipFree(d_tex);
     (void)hipFree(d_status);
     (void)hipDeviceSynchronize();
@@ -356,56 +338,23 @@ struct sfrt_world {
     return SFRT_OK;
   }
 
-  // Before a render_band launch on s: link f into the tile-order chain.
+  // Before a render_band / submit_frame launch on s: link f into the tile-order chain.
   int sched_begin(sfrt::FrameRec& f, hipStream_t s) {
     long long tiles = 0;
     const long long key = tile_order_on ? sfrt::trace_tile_key(f, &tiles) : 0;
-    if (key == 0) return SFRT_OK;  // this launch takes no part (the chain is left as it is)
-    if (tiles > sched.cap) {       // (re)allocate; a new chain starts
-      HIP_TRY(hipDeviceSynchronize());
-      for (int k = 0; k < 2; k++) {
-        (void)hipFree(sched.order[k]);
-        (void)hipFree(sched.cost[k]);
-        sched.order[k] = nullptr;
-        sched.cost[k] = nullptr;
-      }
-      sched.cap = 0;
-      for (int k = 0; k < 2; k++) {
-        HIP_TRY(hipMalloc(&sched.order[k], sizeof(uint32_t) * (size_t)tiles));
-        HIP_TRY(hipMalloc(&sched.cost[k], (size_t)tiles));
-      }
-      if (!sched.last_ev) HIP_TRY(hipEventCreateWithFlags(&sched.last_ev, hipEventDisableTiming));
-      sched.cap = tiles;
-      sched.k = 0;
-      sched.key_prev = 0;
-      sched.sorted_prev = false;
-      sched.have_last = false;
-    }
-    if (sched.have_last && sched.last_stream != s) HIP_TRY(hipStreamWaitEvent(s, sched.last_ev, 0));
-    const int64_t k = sched.k;
-    const bool same = sched.key_prev == key;  // launch k-1 had this tile grid
-    f.tile_order = (same && sched.sorted_prev) ? sched.order[k & 1] : nullptr;
-    f.tile_cost = sched.cost[k & 1];
-    f.prev_cost = same ? sched.cost[(k + 1) & 1] : nullptr;
-    f.next_order = sched.order[(k + 1) & 1];
-    if (tile_order_on == 2 && sched.sorted_prev && same) {
-      // timing probe only: keep dispatching the last order built (by launch k-1), no
-      // sorter, the chain does not advance
-      f.prev_cost = nullptr;
-      return SFRT_OK;
-    }
-    sched.sorted_prev = same;
-    sched.key_prev = key;
-    sched.k = k + 1;
+    sfrt::TileSchedPtrs p;
+    HIP_TRY(sched.begin(key, tiles, s, tile_order_on, p));
+    f.tile_order = p.tile_order;
+    f.tile_cost = p.tile_cost;
+    f.prev_cost = p.prev_cost;
+    f.next_order = p.next_order;
     return SFRT_OK;
   }
 
-  // After a launch that took part in the chain.
   int sched_end(const sfrt::FrameRec& f, hipStream_t s) {
-    if (!f.tile_cost) return SFRT_OK;
-    HIP_TRY(hipEventRecord(sched.last_ev, s));
-    sched.last_stream = s;
-    sched.have_last = true;
+    sfrt::TileSchedPtrs p;
+    p.tile_cost = f.tile_cost;
+    HIP_TRY(sched.end(p, s));
     return SFRT_OK;
   }
 

@@ -58,8 +58,17 @@ struct VoxFrame {
   long long out_pitch;
   uint32_t* out;
   int* status;                              // bit 1: out-of-range texel read
+  int32_t variant;                          // A/B only: 1 = the 2-D grid, no tile order
+  // Adaptive tile order (sfrt_sched.h): one 8x8 tile per one-wave
+  // workgroup, slot -> tile_order; cost = the tile's DDA + shadow-ray steps.
+  const uint32_t* tile_order;
+  uint8_t* tile_cost;
+  const uint8_t* prev_cost;
+  uint32_t* next_order;
 };
 
+// Tile grid of launch_voxel for f (8x8 tiles): key (> 0) and tile count.
+long long voxel_tile_key(const VoxFrame& f, long long* tiles);
 int launch_voxel(const VoxFrame& f, void* stream);
 
 }  // namespace sfrt

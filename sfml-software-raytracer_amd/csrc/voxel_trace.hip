@@ -8,6 +8,7 @@
 // (out-of-range and NaN give INT_MIN / 0) emulated explicitly.
 #include <hip/hip_runtime.h>
 
+#include "sfrt_device.h"
 #include "sfrt_math.h"
 #include "voxel_trace.h"
 
@@ -74,7 +75,7 @@ __device__ __forceinline__ uint32_t pack(uint32_t r, uint32_t g, uint32_t b, uin
 
 // World::LRaycast, World.cpp:455-491.
 template <bool RECIP>
-__device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
+__device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist, uint32_t& work) {
   float dist = 0.0f;
   int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
   const float dirxadd = dir.x > 0 ? 1.0f : 0.0f, diryadd = dir.y > 0 ? 1.0f : 0.0f,
@@ -87,6 +88,7 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
   const float m2 = maxDist * 2;
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
+    work++;
     if (block_at(f, pix, piy, piz) != kVoxEmpty) return false;
     const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
@@ -104,15 +106,16 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
   return dist >= maxDist;
 }
 
-__device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist) {
+__device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist, uint32_t& work) {
   const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
-  if (__builtin_amdgcn_ballot_w64(!ok)) return lraycast_t<false>(f, pos, dir, maxDist);
-  return lraycast_t<true>(f, pos, dir, maxDist);
+  if (__builtin_amdgcn_ballot_w64(!ok)) return lraycast_t<false>(f, pos, dir, maxDist, work);
+  return lraycast_t<true>(f, pos, dir, maxDist, work);
 }
 
 // World::Raycast, World.cpp:302-453.
 template <bool RECIP>
-__device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale, float atan_dir) {
+__device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale, float atan_dir,
+                              uint32_t& work) {
   const V3 cam{f.cam[0], f.cam[1], f.cam[2]};
   float dist = 0.0f;
   V3 pos = cam;
@@ -129,6 +132,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale, float ata
   float raySpeed = 0.0f;
   int colRay = 0;
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
+    work++;
     const float xray = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float yray = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
     const float zray = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
@@ -229,7 +233,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale, float ata
             if (L.shadows && tryDist < f.shadow_distance) {
               dd = __builtin_sqrtf(nx * nx + ny * ny + nz * nz);  // VLength
               nx = nx / dd; ny = ny / dd; nz = nz / dd;
-              lit = lraycast(f, pos, V3{nx, ny, nz}, dd);
+              lit = lraycast(f, pos, V3{nx, ny, nz}, dd, work);
             }
             if (lit) {
               litr += add * L.r;
@@ -247,10 +251,11 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale, float ata
   return pack(0, 0, 0, 255);  // sf::Color::Black
 }
 
-__device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_dir) {
+__device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale, float atan_dir,
+                            uint32_t& work) {
   const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
-  if (__builtin_amdgcn_ballot_w64(!ok)) return raycast_t<false>(f, dir, yscale, atan_dir);
-  return raycast_t<true>(f, dir, yscale, atan_dir);
+  if (__builtin_amdgcn_ballot_w64(!ok)) return raycast_t<false>(f, dir, yscale, atan_dir, work);
+  return raycast_t<true>(f, dir, yscale, atan_dir, work);
 }
 
 // 8x8 pixels per one-wave workgroup (a finished wave's slot refills at once;
@@ -267,17 +272,71 @@ __global__ __launch_bounds__(kVoxTile * kVoxTile) void k_voxel(VoxFrame f) {
   const int i = f.xstart + a * f.xadd;
   const int j = f.ystart + b * f.yadd;
   const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
-  const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2]);
+  uint32_t work = 0;
+  const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
   f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
+}
+
+// The default: 8x8 tiles on a 1-D grid of one-wave workgroups in the adaptive
+// tile order (sfrt_device.h sort_tiles; workgroup 0 is the sorter when
+// prev_cost is set).  Edge lanes run no ray but stay for the wave's reduction.
+__global__ __launch_bounds__(64) void k_voxel_ordered(VoxFrame f, int tiles_x, int ntiles) {
+  const int lane = threadIdx.x & 63;
+  int slot = (int)blockIdx.x;
+  if (f.prev_cost) {
+    if (slot == 0) {
+      sort_tiles(f.prev_cost, ntiles, f.next_order);
+      return;
+    }
+    slot -= 1;
+  }
+  int tile = slot;
+  if (f.tile_order) {
+    const int t = (int)f.tile_order[slot];
+    tile = t < ntiles ? t : slot;  // never outside the grid
+  }
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int a = tx * 8 + (lane & 7);
+  const int b = f.sub_row0 + ty * 8 + (lane >> 3);
+  const bool in = a < f.sub_w && b < f.sub_row0 + f.sub_rows;
+  uint32_t work = 0;
+  if (in) {
+    const int i = f.xstart + a * f.xadd;
+    const int j = f.ystart + b * f.yadd;
+    const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
+    const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
+    f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
+  }
+  if (f.tile_cost) {
+    // the tile's slowest ray, in DDA + shadow steps / 4 (the classes' scale)
+    const uint32_t w = wave_max_u32(work);
+    if (lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket(w >> 2);
+  }
 }
 
 }  // namespace
 
+long long voxel_tile_key(const VoxFrame& f, long long* tiles) {
+  *tiles = 0;
+  if (f.variant == 1 || kVoxTile != 8 || f.sub_w <= 0 || f.sub_rows <= 0) return 0;
+  const long long tx = (f.sub_w + 7) / 8, ty = (f.sub_rows + 7) / 8;
+  *tiles = tx * ty;
+  return (1ll << 62) | (tx << 28) | ty;
+}
+
 int launch_voxel(const VoxFrame& f, void* stream) {
   if (f.sub_w <= 0 || f.sub_rows <= 0) return 0;
-  const dim3 grid((unsigned)((f.sub_w + kVoxTile - 1) / kVoxTile),
-                  (unsigned)((f.sub_rows + kVoxTile - 1) / kVoxTile));
-  hipLaunchKernelGGL(k_voxel, grid, dim3(kVoxTile * kVoxTile), 0, (hipStream_t)stream, f);
+  long long tiles = 0;
+  if (voxel_tile_key(f, &tiles) == 0) {  // A/B: the 2-D grid
+    const dim3 grid((unsigned)((f.sub_w + kVoxTile - 1) / kVoxTile),
+                    (unsigned)((f.sub_rows + kVoxTile - 1) / kVoxTile));
+    hipLaunchKernelGGL(k_voxel, grid, dim3(kVoxTile * kVoxTile), 0, (hipStream_t)stream, f);
+  } else {
+    if (tiles > 0x7ffffffeLL) return -1;
+    const int tiles_x = (f.sub_w + 7) / 8;
+    hipLaunchKernelGGL(k_voxel_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,
+                       (hipStream_t)stream, f, tiles_x, (int)tiles);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

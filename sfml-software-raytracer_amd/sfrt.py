@@ -41,7 +41,7 @@ ABI_SYMBOLS = (
     "sfrt_voxel_set_view", "sfrt_voxel_set_blocks", "sfrt_voxel_load_texture",
     "sfrt_voxel_load_dyn_texture", "sfrt_voxel_set_colors", "sfrt_voxel_set_dynamics",
     "sfrt_voxel_set_lights", "sfrt_voxel_update_image", "sfrt_voxel_render_band",
-    "sfrt_voxel_check",
+    "sfrt_voxel_check", "sfrt_voxel_set_option",
     "sfrt_glsl_create", "sfrt_glsl_destroy", "sfrt_glsl_set_ground", "sfrt_glsl_set_uniforms",
     "sfrt_glsl_get_uniforms", "sfrt_glsl_set_uniform", "sfrt_glsl_set_uniform_int",
     "sfrt_glsl_draw", "sfrt_glsl_draw_image", "sfrt_glsl_check", "sfrt_glsl_set_option",
@@ -136,6 +136,7 @@ def lib() -> ctypes.CDLL:
         "sfrt_voxel_update_image": ([vp, vp, c_int, c_int, c_int, c_int], c_int),
         "sfrt_voxel_render_band": ([vp, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
         "sfrt_voxel_check": ([vp, vp], c_int),
+        "sfrt_voxel_set_option": ([vp, c_int, c_int], c_int),
         "sfrt_glsl_create": ([c_int, P(vp)], c_int),
         "sfrt_glsl_destroy": ([vp], None),
         "sfrt_glsl_set_ground": ([vp, vp, c_int, c_int], c_int),
@@ -437,6 +438,9 @@ class VoxelWorld:
 
     def check(self, stream: int = 0) -> None:
         _check(lib().sfrt_voxel_check(self._h, ctypes.c_void_p(stream or None)), "voxel_check")
+
+    def set_option(self, option: int, value: int) -> None:
+        _check(lib().sfrt_voxel_set_option(self._h, option, value), "voxel_set_option")
 
 
 def decode_png(data: bytes) -> tuple[np.ndarray, int, int]:

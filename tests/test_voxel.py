@@ -112,3 +112,42 @@ def test_voxel_gpu_subsets_and_bands(vworld, assets):
         vworld.render_band(dev[r0].data_ptr(), 320 * 4, r0, r1 - r0, s)
     vworld.check(s)
     assert np.array_equal(dev.cpu().numpy().ravel(), o.render(1))
+
+
+@pytest.mark.gpu
+def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
+    """SFRT_OPT_TILE_ORDER on the voxel renderer: frames rendered back to back through
+    render_band (order from two frames back, poses and sizes changing, a row band) equal
+    the row-major 2-D-grid kernel's frames (SFRT_OPT_VARIANT 1) and the oracle."""
+    import sfrt
+    import torch
+    seq = [((15.5, 1.9, 15.5), 0.0, 0.0, 640, 360, 0, 360)] * 4 + \
+          [((30.25, 2.6, 12.75), 0.3 * k, 0.05 * k, 640, 360, 0, 360) for k in range(4)] + \
+          [((47.5, 1.5, 60.1), 4.0, -0.3, 333, 211, 0, 211)] * 3 + \
+          [((47.5, 1.5, 60.1), 4.0, -0.3, 640, 360, 40, 200)] * 3
+    stream = torch.cuda.Stream()
+    frames = []
+    vworld.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)  # off by default for the voxel renderer
+    with torch.cuda.stream(stream):
+        for p, r, hr, width, height, r0, rows in seq:
+            vworld.set_scene(vs.default_world(p, r, hr), width, height)
+            b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            vworld.render_band(b[r0].data_ptr(), width * 4, r0, rows, stream.cuda_stream)
+            frames.append(b)
+    vworld.check(stream.cuda_stream)
+    torch.cuda.synchronize()
+    vworld.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+    vworld.set_option(sfrt.SFRT_OPT_VARIANT, 1)
+    try:
+        for k, ((p, r, hr, width, height, r0, rows), b) in enumerate(zip(seq, frames)):
+            vworld.set_scene(vs.default_world(p, r, hr), width, height)
+            want = np.full(width * height * 4, 0xA5, dtype=np.uint8)
+            full = vworld.render()
+            want[r0 * width * 4:(r0 + rows) * width * 4] = full[r0 * width * 4:(r0 + rows) * width * 4]
+            assert np.array_equal(b.cpu().numpy().ravel(), want), (k, p, width, height, r0, rows)
+            if k in (0, 11):
+                o = oracle.VoxelOracle(vs.default_world(p, r, hr), width, height, assets[0], assets[1],
+                                       vs.COLORS)
+                assert np.array_equal(full, o.render(host_threads())), k
+    finally:
+        vworld.set_option(sfrt.SFRT_OPT_VARIANT, 0)
