@@ -6,9 +6,10 @@
 // grid) reads order[k % 2] (built by launch k-1 from launch k-2's costs), records
 // its per-tile march-step classes into cost[k % 2], and -- from its extra
 // workgroup 0 -- sorts cost[(k+1) % 2] (launch k-1's) into order[(k+1) % 2].
-// Consecutive launches are ordered by their stream; a launch on another stream
-// than the previous one first waits for it.  An order is used only when the two
-// launches before had the same grid (key).  Scheduling only: every tile is
+// Consecutive launches are ordered by their stream; before a launch on another
+// stream than the previous one, the host waits for the previous one.  An order is
+// used only when the two launches before had the same grid (key).  Scheduling
+// only: every tile is
 // rendered once whatever the order.
 #pragma once
 
@@ -33,7 +34,6 @@ struct TileSched {
   long long key_prev = 0;        // tile grid of launch k-1 (0: none)
   bool sorted_prev = false;      // launch k-1 sorted launch k-2's tiles into order[k % 2]
   hipStream_t last_stream = nullptr;
-  hipEvent_t last_ev = nullptr;
   bool have_last = false;
 
   void release() {
@@ -44,8 +44,6 @@ struct TileSched {
       cost[q] = nullptr;
     }
     cap = 0;
-    if (last_ev) (void)hipEventDestroy(last_ev);
-    last_ev = nullptr;
   }
 
   // Link a launch on s with tile grid `key` (0: takes no part) of `tiles` tiles
@@ -57,23 +55,21 @@ struct TileSched {
     hipError_t e;
     if (tiles > cap) {  // (re)allocate; a new chain starts
       if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
-      hipEvent_t ev = last_ev;
-      last_ev = nullptr;
       release();
-      last_ev = ev;
       for (int q = 0; q < 2; q++) {
         if ((e = hipMalloc(&order[q], sizeof(uint32_t) * (size_t)tiles)) != hipSuccess) return e;
         if ((e = hipMalloc(&cost[q], (size_t)tiles)) != hipSuccess) return e;
       }
-      if (!last_ev && (e = hipEventCreateWithFlags(&last_ev, hipEventDisableTiming)) != hipSuccess)
-        return e;
       cap = tiles;
       k = 0;
       key_prev = 0;
       sorted_prev = false;
       have_last = false;
     }
-    if (have_last && last_stream != s && (e = hipStreamWaitEvent(s, last_ev, 0)) != hipSuccess)
+    // A launch on another stream than the previous one: the host waits for the
+    // previous one (rare; an event recorded after every launch would instead put a
+    // marker between every two frames of the common single-stream loop).
+    if (have_last && last_stream != s && (e = hipStreamSynchronize(last_stream)) != hipSuccess)
       return e;
     const bool same = key_prev == key;  // launch k-1 had this tile grid
     p.tile_order = (same && sorted_prev) ? order[k & 1] : nullptr;
@@ -93,8 +89,6 @@ struct TileSched {
   // After the launch that took part (p.tile_cost set) was queued on s.
   hipError_t end(const TileSchedPtrs& p, hipStream_t s) {
     if (!p.tile_cost) return hipSuccess;
-    const hipError_t e = hipEventRecord(last_ev, s);
-    if (e != hipSuccess) return e;
     last_stream = s;
     have_last = true;
     return hipSuccess;
