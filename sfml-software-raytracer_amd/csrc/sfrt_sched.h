@@ -9,8 +9,7 @@
 // Consecutive launches are ordered by their stream; before a launch on another
 // stream than the previous one, the host waits for the previous one.  An order is
 // used only when the two launches before had the same grid (key).  Scheduling
-// only: every tile is
-// rendered once whatever the order.
+// only: every tile is rendered once whatever the order.
 #pragma once
 
 #include <hip/hip_runtime.h>
