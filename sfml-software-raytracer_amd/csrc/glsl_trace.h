@@ -65,8 +65,16 @@ struct GlslFrame {
   long long out_pitch;                 // in pixels
   uint32_t* out;
   int* status;                         // bit 0: march cap reached
+  // Adaptive tile order (sfrt_sched.h): 8x8 tiles, one per one-wave
+  // workgroup, slot -> tile_order; cost = the tile's longest metaball march.
+  const uint32_t* tile_order;
+  uint8_t* tile_cost;
+  const uint8_t* prev_cost;
+  uint32_t* next_order;
 };
 
+// Tile grid of the ordered GLSL kernel for f: key (> 0) and tile count.
+long long glsl_tile_key(const GlslFrame& f, long long* tiles);
 int launch_glsl(const GlslFrame& f, void* stream);
 
 }  // namespace sfrt

@@ -14,6 +14,7 @@
 
 #include "glsl_trace.h"
 #include "sfrt_device.h"
+#include "sfrt_device.h"
 #include "sfrt_math.h"
 
 #pragma clang fp contract(off)
@@ -52,7 +53,8 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
 
 template <bool LDS>
 __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __restrict__ walls,
-                                         const GlslBall* __restrict__ balls, int i, int row) {
+                                         const GlslBall* __restrict__ balls, int i, int row,
+                                         uint32_t& work, bool store = true) {
   const float fx = (float)i + 0.5f;
   const float fy = (float)(f.height - 1 - row) + 0.5f;
   const float ax = -f.fov_x + f.hk * fx;                                   // :172-173
@@ -154,6 +156,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
     }
     ball_dist += smooth + 0.01f;
   }
+  work = (uint32_t)steps;
 
   // ---- wall or ball (:114-120) ----
   const int wall = smooth < 0.01f ? 0 : 1;
@@ -237,8 +240,9 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
   cr *= fog;
   cg *= fog;
   cbl *= fog;
-  f.out[(long long)(row - f.row0) * f.out_pitch + i] =
-      unorm8(cr) | (unorm8(cg) << 8) | (unorm8(cbl) << 16) | (255u << 24);
+  if (store)
+    f.out[(long long)(row - f.row0) * f.out_pitch + i] =
+        unorm8(cr) | (unorm8(cg) << 8) | (unorm8(cbl) << 16) | (255u << 24);
 }
 
 // Wall and ball records are read once per visit by every wave, with scalar
@@ -260,15 +264,63 @@ __global__ __launch_bounds__(64 * WPB) void k_glsl(GlslFrame f) {
   const int i = tx * 8 + (lane & 7);
   const int r = ty * 8 + (lane >> 3);
   if (i >= f.width || r >= f.rows) return;
-  fragment<LDS>(f, LDS ? s_walls : f.walls, LDS ? s_balls : f.balls, i, f.row0 + r);
+  uint32_t work = 0;
+  fragment<LDS>(f, LDS ? s_walls : f.walls, LDS ? s_balls : f.balls, i, f.row0 + r, work);
+}
+
+// One 8x8 tile per one-wave workgroup in the adaptive tile order (sfrt_device.h
+// sort_tiles; workgroup 0 is the sorter when prev_cost is set).  Edge lanes run
+// no fragment but stay for the wave's reduction.
+__global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
+  const int lane = threadIdx.x & 63;
+  int slot = (int)blockIdx.x;
+  if (f.prev_cost) {
+    if (slot == 0) {
+      sort_tiles(f.prev_cost, ntiles, f.next_order);
+      return;
+    }
+    slot -= 1;
+  }
+  int tile = slot;
+  if (f.tile_order) {
+    const int t = (int)f.tile_order[slot];
+    tile = t < ntiles ? t : slot;  // never outside the grid
+  }
+  const int tx = tile % f.tiles_x, ty = tile / f.tiles_x;
+  const int i = tx * 8 + (lane & 7);
+  const int r = ty * 8 + (lane >> 3);
+  // Edge lanes shade a clamped duplicate pixel and store nothing: a divergent
+  // branch around fragment() would cost its wave-uniform skips their uniformity.
+  const bool in = i < f.width && r < f.rows;
+  uint32_t work = 0;
+  fragment<false>(f, f.walls, f.balls, i < f.width ? i : f.width - 1,
+                  f.row0 + (r < f.rows ? r : f.rows - 1), work, in);
+  if (f.tile_cost) {
+    const uint32_t w = wave_max_u32(work);  // the tile's longest march
+    if (lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket(w);
+  }
 }
 
 }  // namespace
+
+long long glsl_tile_key(const GlslFrame& f, long long* tiles) {
+  *tiles = 0;
+  if (f.variant != 0 || f.tiles_x <= 0 || f.rows <= 0) return 0;
+  const long long ty = (f.rows + 7) / 8;
+  *tiles = (long long)f.tiles_x * ty;
+  return (1ll << 62) | ((long long)f.tiles_x << 28) | ty;
+}
 
 int launch_glsl(const GlslFrame& f, void* stream) {
   const int tiles_y = (f.rows + 7) / 8;
   const long long tiles = (long long)f.tiles_x * tiles_y;
   if (tiles == 0) return 0;
+  if (f.tile_cost) {  // adaptive tile order (the host linked this launch into its chain)
+    if (tiles > 0x7ffffffeLL) return -1;
+    hipLaunchKernelGGL(k_glsl_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,
+                       (hipStream_t)stream, f, (int)tiles);
+    return hipGetLastError() != hipSuccess;
+  }
   const dim3 g((unsigned)((tiles + 3) / 4)), b(256);
   if (f.variant == 1)
     hipLaunchKernelGGL(k_glsl<true>, g, b, 0, (hipStream_t)stream, f);

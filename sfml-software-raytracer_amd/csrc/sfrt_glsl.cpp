@@ -19,6 +19,7 @@
 
 #include "glsl_trace.h"
 #include "sfrt.h"
+#include "sfrt_sched.h"
 #include "sfrt_math.h"
 
 #pragma clang fp contract(off)
@@ -108,6 +109,8 @@ struct sfrt_glsl {
   sfrt_glsl_uniforms u{};
   int ground_w = 0, ground_h = 0;
   int variant = 0;                     // SFRT_OPT_VARIANT (tuning A/B)
+  int tile_order_on = 0;               // SFRT_OPT_TILE_ORDER (sfrt_glsl_draw): off by default, slower here
+  sfrt::TileSched sched;               // adaptive tile order (sfrt_sched.h)
   // device resources
   hipStream_t stream = nullptr;
   uint32_t* d_mip = nullptr;
@@ -137,6 +140,7 @@ struct sfrt_glsl {
     DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
     (void)hipDeviceSynchronize();
+    sched.release();
     (void)hipFree(d_mip);
     for (auto& t : slots) {
       (void)hipFree(t.d);
@@ -456,7 +460,16 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
   f.tiles_x = (width + 7) / 8;
   f.out = (uint32_t*)dev_pixels;
   f.out_pitch = pitch_bytes / 4;
+  long long tiles = 0;
+  const long long key = g->tile_order_on ? sfrt::glsl_tile_key(f, &tiles) : 0;
+  sfrt::TileSchedPtrs p;
+  HIP_TRY(g->sched.begin(key, tiles, s, g->tile_order_on, p));
+  f.tile_order = p.tile_order;
+  f.tile_cost = p.tile_cost;
+  f.prev_cost = p.prev_cost;
+  f.next_order = p.next_order;
   if (sfrt::launch_glsl(f, s)) return SFRT_E_HIP;
+  HIP_TRY(g->sched.end(p, s));
   return g->launched(s);
 }
 
@@ -494,6 +507,10 @@ int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value) {
   std::lock_guard<std::mutex> lk(g->mu);
   if (option == SFRT_OPT_VARIANT) {
     g->variant = value;
+    return SFRT_OK;
+  }
+  if (option == SFRT_OPT_TILE_ORDER) {
+    g->tile_order_on = value == 2 ? 2 : value ? 1 : 0;
     return SFRT_OK;
   }
   return SFRT_E_INVALID;

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kVoxTile * kVoxTile) void k_voxel(VoxFrame f) {
 
 // The default: 8x8 tiles on a 1-D grid of one-wave workgroups in the adaptive
 // tile order (sfrt_device.h sort_tiles; workgroup 0 is the sorter when
-// prev_cost is set).  Edge lanes run no ray but stay for the wave's reduction.
+// prev_cost is set).
 __global__ __launch_bounds__(64) void k_voxel_ordered(VoxFrame f, int tiles_x, int ntiles) {
   const int lane = threadIdx.x & 63;
   int slot = (int)blockIdx.x;
@@ -298,15 +298,17 @@ __global__ __launch_bounds__(64) void k_voxel_ordered(VoxFrame f, int tiles_x, i
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int a = tx * 8 + (lane & 7);
   const int b = f.sub_row0 + ty * 8 + (lane >> 3);
+  // Edge lanes trace a clamped duplicate pixel and store nothing (a divergent
+  // branch around raycast() would make its wave-uniform choices divergent).
   const bool in = a < f.sub_w && b < f.sub_row0 + f.sub_rows;
+  const int ac = a < f.sub_w ? a : f.sub_w - 1;
+  const int bc = b < f.sub_row0 + f.sub_rows ? b : f.sub_row0 + f.sub_rows - 1;
   uint32_t work = 0;
-  if (in) {
-    const int i = f.xstart + a * f.xadd;
-    const int j = f.ystart + b * f.yadd;
-    const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
-    const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
-    f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
-  }
+  const int i = f.xstart + ac * f.xadd;
+  const int j = f.ystart + bc * f.yadd;
+  const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
+  const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
+  if (in) f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
   if (f.tile_cost) {
     // the tile's slowest ray, in DDA + shadow steps / 4 (the classes' scale)
     const uint32_t w = wave_max_u32(work);

@@ -339,3 +339,38 @@ def test_gpu_errors_fail_loudly(built, floor):
     s.set_uniforms(u)
     assert s.draw_image(64, 64).size == 64 * 64 * 4
     s.close()
+
+
+@pytest.mark.gpu
+def test_gpu_adaptive_tile_order_same_bytes(shader, floor):
+    """SFRT_OPT_TILE_ORDER on the GLSL renderer (sfrt_glsl_draw dispatches 8x8 tiles
+    longest-first by the metaball-march steps of two frames back): frames drawn back to back
+    on one stream -- static uniforms, moving ospheres, size changes, a row band -- equal
+    draw_image's frames (the row-major kernel) and, for two of them, the oracle."""
+    import torch
+    seq = [(gs.default_uniforms(640, 360, 0.0, 0.0), 640, 360, 0, 360)] * 4 + \
+          [(gs.default_uniforms(640, 360, 0.3 * k, 0.1, frames=20 * k), 640, 360, 0, 360)
+           for k in range(4)] + \
+          [(gs.random_uniforms(3, 40, 4, 50, 333, 211), 333, 211, 0, 211)] * 3 + \
+          [(gs.default_uniforms(640, 360, 2.5, -0.2), 640, 360, 40, 200)] * 3
+    import sfrt
+    stream = torch.cuda.Stream()
+    frames = []
+    shader.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)  # off by default for the GLSL renderer
+    with torch.cuda.stream(stream):
+        for u, w, h, r0, rows in seq:
+            shader.set_uniforms(u)
+            b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            shader.draw(b[r0].data_ptr(), w, h, w * 4, r0, rows, stream.cuda_stream)
+            frames.append(b)
+    shader.check(stream.cuda_stream)
+    torch.cuda.synchronize()
+    shader.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+    for k, ((u, w, h, r0, rows), b) in enumerate(zip(seq, frames)):
+        full = draw(shader, u, w, h)
+        want = np.full(w * h * 4, 0xA5, dtype=np.uint8)
+        want[r0 * w * 4:(r0 + rows) * w * 4] = full[r0 * w * 4:(r0 + rows) * w * 4]
+        got = b.cpu().numpy().ravel()
+        assert np.array_equal(got, want), (k, first_diff(got, want, w))
+        if k in (3, 10):
+            assert np.array_equal(full, oracle.GlslOracle(u, *floor).render(w, h, host_threads())), k

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--variants", default="0", help="SFRT_OPT_VARIANT values to time")
+    ap.add_argument("--orders", default="1",
+                    help="SFRT_OPT_TILE_ORDER values (1 adaptive, 0 row-major; keys get /o0)")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -41,9 +43,13 @@ def main():
         s.set_uniforms(u)
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
         for var in [int(v) for v in args.variants.split(",")]:
-            s.set_option(sfrt.SFRT_OPT_VARIANT, var)
-            res.update(time_one(s, buf, width, height, u, rot, frames, var, args, stream, floor,
-                                threads, oracle))
+            for order in [int(v) for v in args.orders.split(",")]:
+                s.set_option(sfrt.SFRT_OPT_VARIANT, var)
+                s.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+                r = time_one(s, buf, width, height, u, rot, frames, var, args, stream, floor,
+                             threads, oracle)
+                res.update({(k + ("" if order else "/o0")): v for k, v in r.items()})
+        s.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
     print(json.dumps(res, indent=1))
 
 
