@@ -635,6 +635,9 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
 // kFlBits -- the visit loop clears each visited bit with s_bitset0_b64.
 constexpr int kFlMask = 1, kFlFree = 2, kFlPrefetch = 4, kFlPair = 8, kFlNoShade = 32,
               kFlNoTiny = 64, kFlBits = 128;
+// kFlVisitCost -- the tile-order cost is the wave's sphere visits (slots + window
+// bits, summed in SALU), not its march steps.
+constexpr int kFlVisitCost = 256;
 constexpr int kFlDefault = kFlMask | kFlFree | kFlNoTiny;
 
 template <int SLOTS, int R, int WPB, int TLO_EVERY = 1, int FL = 0>
@@ -731,6 +734,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     pass_body_r<R, (FL & kFlNoTiny) != 0>(ss, s_pass, rad, k, L, dnew);
   };
   int trips = 1;
+  uint32_t visits = 0;  // kFlVisitCost: wave-uniform (SGPR) sum of the sphere visits
   if (SLOTS > 0 && windowed && __builtin_popcountll(m) <= SLOTS) {
     constexpr int NS = SLOTS > 0 ? SLOTS : 1;
     float scx[NS], scy[NS], scz[NS], sr[NS], ssp[NS];
@@ -768,6 +772,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         const SphereRec& s = sph[k];
         visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
       }
+      if (FL & kFlVisitCost) visits += (uint32_t)SLOTS + (uint32_t)__builtin_popcountll(rest);
       advance(L, dnew);
     }
   } else {
@@ -799,6 +804,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         const float thi = __uint_as_float(wave_max_u32(th));
         win = m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
       }
+      if (FL & kFlVisitCost) visits += (uint32_t)__builtin_popcountll(win);
       float L[R];
       int dnew[R];
 #pragma unroll
@@ -855,7 +861,8 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
   }
   if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
-  if (WPB == 1 && f.tile_cost && lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket((uint32_t)trips);
+  if (WPB == 1 && f.tile_cost && lane == 0)
+    f.tile_cost[tile] = (uint8_t)tile_bucket((FL & kFlVisitCost) ? (visits >> 2) : (uint32_t)trips);
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (valid[r]) {
@@ -1037,20 +1044,32 @@ __global__ __launch_bounds__(256) void k_trace_points(FrameRec f, const int* __r
 
 }  // namespace
 
+// Pixels per lane of an ordered launch (adaptive tile order): three (24x8
+// tiles) once that grid still has >= 32768 tiles -- four waves per wave slot of
+// the chip, enough for longest-first to balance (4K, 64 spheres: 177 -> 172.5
+// us) -- else two (16x8; 1080p, 10 spheres: 37.3 us against 39.4 with 24x8).
+static int ordered_rays(const FrameRec& f) {
+  const long long t3 = (long long)((f.sub_w + 3 * kTile - 1) / (3 * kTile)) *
+                       ((f.sub_rows + kTile - 1) / kTile);
+  return t3 >= 32768 ? 3 : 2;
+}
+
 // The kernel choice of launch_trace, shared with trace_tile_key.  Default:
-// two pixels per lane (16x8 tiles) above kPairMinSpheres spheres, and for any
-// scene when the launch is in the adaptive tile order (1080p, 10 spheres:
-// 42.0 -> 37.4 us; without the order the 8x8 tiles win there, 45.7 vs 48.5).
+// two pixels per lane (16x8 tiles) above kPairMinSpheres spheres; in the
+// adaptive tile order ordered_rays for any scene (1080p, 10 spheres: 16x8 tiles
+// 37.4 us against 42.0 with 8x8, which win only in row-major order: 45.7 vs 48.5).
 static int trace_rays(const FrameRec& f, bool ordered) {
   return f.variant == 49 ? 1
          : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
-         : f.variant == 72 ? 3
-         : f.variant == 73 ? 4
+         : f.variant == 72 || f.variant == 85 ? 3
+         : f.variant == 73 || f.variant == 86 ? 4
          : f.variant == 74 || f.variant == 75 || f.variant == 83 || f.variant == 91 ? 1
-         : (f.variant >= 60 && f.variant <= 71) || (f.variant >= 80 && f.variant <= 82) || f.variant == 90 ? 2
+         : (f.variant >= 60 && f.variant <= 71) || (f.variant >= 80 && f.variant <= 82) || f.variant == 84 ||
+                f.variant == 90 ? 2
          : f.variant == 42 ? 3
          : f.variant == 43 ? 4
-         : (f.variant == 0 && (f.n > kPairMinSpheres || ordered)) ? 2 : 1;
+         : (f.variant == 0 && ordered) ? ordered_rays(f)
+         : (f.variant == 0 && f.n > kPairMinSpheres) ? 2 : 1;
 }
 static bool trace_window_r(const FrameRec& f, int rays) {
   return f.n <= kInlineSpheres &&
@@ -1133,6 +1152,11 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
       case 82:
         hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, 3 | kFlNoTiny | kFlBits>), g1, b1, 0, s, args);
         break;
+      case 84:
+        hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault | kFlVisitCost>), g1, b1, 0, s, args);
+        break;
+      case 85: hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 2, kFlDefault>), g1, b1, 0, s, args); break;
+      case 86: hipLaunchKernelGGL((k_trace_window_r<kSlots, 4, 1, 2, kFlDefault>), g1, b1, 0, s, args); break;
       case 90: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault | kFlNoShade>), g1, b1, 0, s, args); break;
       case 91: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlDefault | kFlNoShade>), g1, b1, 0, s, args); break;
       case 47: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2>), g1, b1, 0, s, args); break;
@@ -1142,6 +1166,8 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
       default:
         if (rays == 1)  // default for n <= kPairMinSpheres: 8x8 tiles (= variant 83)
           hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlDefault>), g1, b1, 0, s, args);
+        else if (rays == 3)  // large ordered frames (= variant 85)
+          hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 2, kFlDefault>), g1, b1, 0, s, args);
         else  // (= variant 80)
           hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault>), g1, b1, 0, s, args);
         break;
