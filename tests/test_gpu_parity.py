@@ -479,3 +479,33 @@ def test_adaptive_tile_order_4k_frames(world, floor):
     torch.cuda.synchronize()
     for k, (p, b) in enumerate(frames):
         assert torch.equal(b, rowmajor[p]), (k, p)
+
+
+def test_adaptive_order_ragged_24x8_tiles(world, floor):
+    """A large ragged frame (3333 x 2111: >= 32768 tiles of 24x8, three pixels per lane, edge
+    lanes in both directions) through the ordered render_band path, four frames back to back
+    with two poses: every frame equals update_image's (the row-major 16x8 kernel) bytes, and
+    one of them the oracle's."""
+    import torch
+    width, height = 3333, 2111
+    poses = [(0.4, 0.1), (2.0, -0.3)]
+    want = {}
+    for p in poses:
+        world.set_scene(scenes.lcg64().posed(*p), width, height)
+        want[p] = world.render()
+    stream = torch.cuda.Stream()
+    frames = []
+    with torch.cuda.stream(stream):
+        for k in range(4):
+            p = poses[k // 2]
+            world.set_scene(scenes.lcg64().posed(*p), width, height)
+            b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+            frames.append((p, b))
+    world.check(stream.cuda_stream)
+    torch.cuda.synchronize()
+    for k, (p, b) in enumerate(frames):
+        assert diff_report(b.cpu().numpy().ravel(), want[p], width) == "", (k, p)
+    sc = scenes.lcg64().posed(*poses[1])
+    assert diff_report(want[poses[1]], oracle_for(sc, width, height, floor).render(host_threads()),
+                       width) == ""
