@@ -214,8 +214,8 @@ SFRT_API int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pit
 SFRT_API int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream);
 /* SFRT_OPT_TILE_ORDER as for sfrt_world, but off (0) by default here: render_band with 1
  * dispatches 8x8 tiles longest-first by the DDA + shadow steps of two frames back (same
- * bytes; measured 1-6% slower on the voxel worlds); SFRT_OPT_VARIANT 1 = the
- * 2-D-grid kernel (A/B). */
+ * bytes; measured 1-6% slower on the voxel worlds); SFRT_OPT_VARIANT (A/B,
+ * same bytes): 1 = the 2-D-grid kernel, 3 = the grid's occupancy bitmask staged in LDS. */
 SFRT_API int sfrt_voxel_set_option(sfrt_voxel* v, int option, int value);
 
 /* ======================================================================

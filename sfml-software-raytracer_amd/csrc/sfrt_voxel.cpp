@@ -90,6 +90,9 @@ struct sfrt_voxel {
   DevTex tex[sfrt::kVoxSlots], dyn_tex[sfrt::kVoxSlots];
   int16_t* d_blocks = nullptr;
   size_t d_blocks_cap = 0;
+  uint32_t* d_occ = nullptr;   // 1 bit per dense cell: non-empty (LDS-staged by the kernel)
+  size_t d_occ_cap = 0;
+  int occ_words = 0;
   bool blocks_dirty = true;
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
@@ -122,6 +125,7 @@ struct sfrt_voxel {
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
     (void)hipFree(d_blocks);
+    (void)hipFree(d_occ);
     for (auto& t : slots) {
       (void)hipFree(t.d);
       (void)hipHostFree(t.h);
@@ -223,11 +227,27 @@ struct sfrt_voxel {
       }
       HIP_TRY(hipMemcpy(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
                         hipMemcpyHostToDevice));
+      // occupancy bitmask of the dense grid, index (x * ny + y) * nz + z
+      const size_t words = (blocks.size() + 31) / 32;
+      std::vector<uint32_t> occ(words, 0u);
+      for (size_t c = 0; c < blocks.size(); c++)
+        if (blocks[c] != sfrt::kVoxEmpty) occ[c >> 5] |= 1u << (c & 31);
+      if (d_occ_cap < words) {
+        (void)hipFree(d_occ);
+        d_occ = nullptr;
+        d_occ_cap = 0;
+        HIP_TRY(hipMalloc(&d_occ, words * sizeof(uint32_t)));
+        d_occ_cap = words;
+      }
+      HIP_TRY(hipMemcpy(d_occ, occ.data(), words * sizeof(uint32_t), hipMemcpyHostToDevice));
+      occ_words = (int)words;
       blocks_dirty = false;
     }
     f.col = (const float*)d;
     f.row = (const float*)(d + b_col);
     f.blocks = d_blocks;
+    f.occ = d_occ;
+    f.occ_words = occ_words;
     f.nx = nx; f.ny = ny; f.nz = nz;
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
       f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};

@@ -151,3 +151,22 @@ def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
                 assert np.array_equal(full, o.render(host_threads())), k
     finally:
         vworld.set_option(sfrt.SFRT_OPT_VARIANT, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [1, 3])
+def test_voxel_kernel_variants_identical(vworld, assets, variant):
+    """SFRT_OPT_VARIANT on the voxel renderer (1: the 2-D-grid kernel; 3: the grid's occupancy
+    bitmask staged in LDS) produces the default kernel's bytes."""
+    import sfrt
+    for case in [(640, 360, (15.5, 1.9, 15.5), 0.0, 0.0), (333, 211, (47.5, 1.5, 60.1), 4.0, -0.3),
+                 (1920, 1080, (30.25, 2.6, 12.75), 2.2, 0.25)]:
+        w, h, p, r, hr = case
+        vworld.set_scene(vs.default_world(p, r, hr), w, h)
+        a = vworld.render()
+        vworld.set_option(sfrt.SFRT_OPT_VARIANT, variant)
+        try:
+            b = vworld.render()
+        finally:
+            vworld.set_option(sfrt.SFRT_OPT_VARIANT, 0)
+        assert np.array_equal(a, b), case
