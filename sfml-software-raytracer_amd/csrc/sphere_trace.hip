@@ -1061,7 +1061,7 @@ static int ordered_rays(const FrameRec& f) {
 static int trace_rays(const FrameRec& f, bool ordered) {
   return f.variant == 49 ? 1
          : f.variant == 40 || f.variant == 41 || (f.variant >= 44 && f.variant <= 48 && f.variant != 46) ? 2
-         : f.variant == 72 || f.variant == 85 ? 3
+         : f.variant == 72 || f.variant == 85 || (f.variant >= 94 && f.variant <= 97) ? 3
          : f.variant == 73 || f.variant == 86 ? 4
          : f.variant == 74 || f.variant == 75 || f.variant == 83 || f.variant == 91 ? 1
          : (f.variant >= 60 && f.variant <= 71) || (f.variant >= 80 && f.variant <= 82) || f.variant == 84 ||
@@ -1157,6 +1157,10 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
         break;
       case 85: hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 2, kFlDefault>), g1, b1, 0, s, args); break;
       case 86: hipLaunchKernelGGL((k_trace_window_r<kSlots, 4, 1, 2, kFlDefault>), g1, b1, 0, s, args); break;
+      case 94: hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 1, kFlDefault>), g1, b1, 0, s, args); break;
+      case 95: hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 4, kFlDefault>), g1, b1, 0, s, args); break;
+      case 96: hipLaunchKernelGGL((k_trace_window_r<0, 3, 1, 2, kFlDefault>), g1, b1, 0, s, args); break;
+      case 97: hipLaunchKernelGGL((k_trace_window_r<8, 3, 1, 2, kFlDefault>), g1, b1, 0, s, args); break;
       case 90: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault | kFlNoShade>), g1, b1, 0, s, args); break;
       case 91: hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlDefault | kFlNoShade>), g1, b1, 0, s, args); break;
       case 47: hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2>), g1, b1, 0, s, args); break;

@@ -96,7 +96,7 @@ def test_cull_on_off_identical(world, floor):
 
 
 @pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 35, 36, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 52,
-                                     61, 62, 63, 64, 67, 71, 72, 73, 74, 75, 80, 81, 82, 83, 84, 85, 86])
+                                     61, 62, 63, 64, 67, 71, 72, 73, 74, 75, 80, 81, 82, 83, 84, 85, 86, 94, 95, 96, 97])
 def test_kernel_variants_identical(world, floor, variant):
     """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
     produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
