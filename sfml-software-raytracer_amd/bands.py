@@ -8,7 +8,7 @@ and the bands travel to rank 0 over RCCL -- the path's one exchange step.
 Two things shape the partition on MI355X:
 
 * rank 0's own band never crosses a link, every other band does.  A 4K
-  band renders at ~33 Grays/s (0.03 ns per pixel) but crosses one xGMI link
+  band renders at ~48 Grays/s (0.021 ns per pixel) but crosses one xGMI link
   at 4 B per pixel (~0.06 ns per pixel at ~65 GB/s one way), so with equal
   bands every rank but 0 idles on its link.  ``root_weighted_spans`` gives
   rank 0 ``factor`` times the rows of each other rank;
