@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--orders", default="1",
                     help="comma list of SFRT_OPT_TILE_ORDER values (1 adaptive, 0 row-major); "
                          "keys get /o0 for row-major")
+    ap.add_argument("--big", action="store_true", help="add the 7680x4320 frame")
     args = ap.parse_args()
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
@@ -57,7 +58,10 @@ def main():
     cases = [("4k_lcg64", 3840, 2160, scenes.lcg64()),
              ("4k_lcg64_rot", 3840, 2160, scenes.lcg64().posed(1.1, -0.2)),
              ("1080_default10", 1920, 1080, scenes.default10())]
-    buf = torch.empty(2160, 3840 * 4, dtype=torch.uint8, device="cuda")
+    if args.big:
+        cases.append(("8k_lcg64", 7680, 4320, scenes.lcg64()))
+    buf = torch.empty(4320 if args.big else 2160, (7680 if args.big else 3840) * 4,
+                      dtype=torch.uint8, device="cuda")
     for rnd in range(args.rounds):
         for name, width, height, sc in cases:
             outside = scenes.Scene(sc.name, sc.spheres, cam_pos=(0.0, 200.0, 0.0),
