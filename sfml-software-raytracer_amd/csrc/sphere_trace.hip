@@ -1044,14 +1044,17 @@ __global__ __launch_bounds__(256) void k_trace_points(FrameRec f, const int* __r
 
 }  // namespace
 
-// Pixels per lane of an ordered launch (adaptive tile order): three (24x8
-// tiles) once that grid still has >= 32768 tiles -- four waves per wave slot of
-// the chip, enough for longest-first to balance (4K, 64 spheres: 177 -> 172.5
-// us) -- else two (16x8; 1080p, 10 spheres: 37.3 us against 39.4 with 24x8).
+// Pixels per lane of an ordered launch (adaptive tile order): the widest tile
+// -- four pixels per lane (32x8), else three (24x8) -- whose grid still has
+// >= 30000 tiles, about four waves per wave slot of the chip, enough for
+// longest-first to balance; else two (16x8).  Measured: 4K 64 spheres 177
+// (16x8) -> 173.5 (24x8) -> 172.9 us (32x8), 8K 645.6 -> 636.7 us (24x8 ->
+// 32x8); 1080p 10 spheres 37.3 us at 16x8 against 39.4 / 41.0 wider.
 static int ordered_rays(const FrameRec& f) {
-  const long long t3 = (long long)((f.sub_w + 3 * kTile - 1) / (3 * kTile)) *
-                       ((f.sub_rows + kTile - 1) / kTile);
-  return t3 >= 32768 ? 3 : 2;
+  const long long rows = (f.sub_rows + kTile - 1) / kTile;
+  const long long t4 = (long long)((f.sub_w + 4 * kTile - 1) / (4 * kTile)) * rows;
+  const long long t3 = (long long)((f.sub_w + 3 * kTile - 1) / (3 * kTile)) * rows;
+  return t4 >= 30000 ? 4 : t3 >= 30000 ? 3 : 2;
 }
 
 // The kernel choice of launch_trace, shared with trace_tile_key.  Default:
@@ -1172,6 +1175,8 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
           hipLaunchKernelGGL((k_trace_window_r<kSlots, 1, 1, 2, kFlDefault>), g1, b1, 0, s, args);
         else if (rays == 3)  // large ordered frames (= variant 85)
           hipLaunchKernelGGL((k_trace_window_r<kSlots, 3, 1, 2, kFlDefault>), g1, b1, 0, s, args);
+        else if (rays == 4)  // larger ordered frames (= variant 86)
+          hipLaunchKernelGGL((k_trace_window_r<kSlots, 4, 1, 2, kFlDefault>), g1, b1, 0, s, args);
         else  // (= variant 80)
           hipLaunchKernelGGL((k_trace_window_r<kSlots, 2, 1, 2, kFlDefault>), g1, b1, 0, s, args);
         break;
