@@ -64,9 +64,9 @@ def measured_traffic(pixels: int):
         if doc.get("kernel", "k_trace") != "k_trace":
             continue
         table = doc.get("per_launch_pixels", doc.get("per_grid_threads", {}))
-        # the steady-state launch has the tile-order sorter workgroup (+64 x R pixels, R = 3,
-        # 2 or 1 pixels per lane)
-        for extra in (192, 128, 64, 0):
+        # the steady-state launch has the tile-order sorter workgroup (+64 x R pixels, R = 4,
+        # 3, 2 or 1 pixels per lane)
+        for extra in (256, 192, 128, 64, 0):
             ent = table.get(str(pixels + extra))
             if ent:
                 return ent, os.path.relpath(path, ROOT)
