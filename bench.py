@@ -76,10 +76,24 @@ def measured_traffic(pixels: int):
 EVENT_EVERY = 8  # frames per HIP-event-timed frame in time_frames
 
 
+def event_pair_ms(stream, n: int = 64) -> float:
+    """Median elapsed time of an empty HIP-event pair on `stream`: the marker overhead that
+    each sampled (start, end) pair adds to the kernel it brackets (subtracted from kernel_ms,
+    so that it agrees with the rocprofv3 kernel trace and never exceeds the wall time per
+    frame)."""
+    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(n)]
+    for a, b in pairs:
+        a.record(stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in pairs]))
+
+
 def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream, per_frame=None):
     """Warmup, then `steps` timed frames through the pipeline.  Returns (wall seconds,
     kernel ms per frame from HIP events around every EVENT_EVERY-th render on the launch
-    stream).
+    stream, minus the empty event pair's own elapsed time).
     per_frame(k), if given, runs before frame k is queued (a moving camera)."""
     for k in range(warmup):
         if per_frame:
@@ -115,7 +129,8 @@ def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream, per_fra
         dist.barrier()
     wall = time.perf_counter() - t0
     world.check(stream.cuda_stream)
-    kernel_ms = sum(starts[k].elapsed_time(ends[k]) for k in sampled) / len(sampled)
+    raw = sum(starts[k].elapsed_time(ends[k]) for k in sampled) / len(sampled)
+    kernel_ms = max(0.0, raw - event_pair_ms(stream))
     return wall, kernel_ms
 
 
@@ -171,10 +186,28 @@ EXTRA_FRAMES = {1: [(7680, 4320)], 2: [(7680, 4320)], 4: [(7680, 4320)],
                 8: [(7680, 4320), (16384, 16384)]}
 
 
+def host_cpu_info() -> dict:
+    """Host CPUs as this process sees them: nproc (the affinity mask), os.cpu_count() (the
+    machine) and the cgroup CPU quota when one is set (the GPU box's share)."""
+    info = {"nproc": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            info["cgroup_cpu_quota"] = round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
 def cpu_baseline(scene, width, height, floor, gpu_frame):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU restatement, timed as the baseline
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cpus = host_cpu_info()
+    # SURVEY 8d: T = nproc threads -- capped at the cgroup CPU quota where one is set (the GPU
+    # box: nproc 256, quota 16), since more threads than the quota only time-slice
+    threads = cpus["nproc"]
+    if "cgroup_cpu_quota" in cpus:
+        threads = max(1, min(threads, int(cpus["cgroup_cpu_quota"])))
     o = oracle.Oracle.from_scene(scene, width, height, *floor)
     t0 = time.perf_counter()
     frame = o.render(threads)
@@ -192,6 +225,7 @@ def cpu_baseline(scene, width, height, floor, gpu_frame):
             "sample": f"one full {width}x{height} frame of the same scene, oracle/sphereworld_oracle.c "
                       f"(-O2, no FMA), {threads} threads with the reference's row interleave "
                       f"(Source.cpp:21), {dt:.2f} s",
+            "host_cpus": cpus,
             "frame_bit_identical_to_gpu": same,
             "single_thread": {"value": round(width * rows1 / dt1 / 1e6, 3), "unit": "Mrays/s",
                               "cores": 1, "sample": f"rows j % 16 == 0 ({rows1} rows), {dt1:.2f} s",
@@ -263,6 +297,7 @@ def main() -> None:
                                    + (" + RCCL transfer to rank 0 (overlapped, bands tuned)"
                                       if world_size > 1 else ""),
                        "width": WIDTH, "height": height, "spheres": int(scene.spheres.shape[0]),
+                       "camera": "static pose (0,0); moving-camera lines under also",
                        "parallelism": f"row-bands x{world_size}"},
             "kernel_ms": round(kernel_ms, 4),
             "bands": bands,
@@ -330,25 +365,38 @@ def main() -> None:
         del pipe3
         # The adaptive tile order dispatches each frame's tiles longest-first
         # by the march steps two frames back.  The same workload with a camera turning every
-        # frame (the order always two poses stale), and in plain row-major order.
+        # frame (the order always two poses stale), in both orders, and the static camera in
+        # plain row-major order.  Only the camera changes per frame (one C-ABI call).
         pipe4 = BandPipeline(0, 1, height, pitch, "cuda")
 
         def turn(k):
-            w.set_scene(scene.posed(0.004 * k, 0.0), WIDTH, height)
-        wall4, k4 = time_frames(w, pipe4, pitch, args.steps, args.warmup, stream, per_frame=turn)
-        result["also"]["3840x2160_lcg64_turning"] = {
-            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall4 / 1e6, 2),
-            "fps": round(args.steps / wall4, 2), "kernel_ms": round(k4, 4),
-            "camera": "rotation += 0.004 rad per frame from 0"}
-        w.set_scene(scene, WIDTH, height)
-        w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
-        wall5, k5 = time_frames(w, pipe4, pitch, args.steps, args.warmup, stream)
+            w.set_camera(scene.cam_pos, 0.004 * k, 0.0)
+        for order, key in ((1, "3840x2160_lcg64_turning"), (0, "3840x2160_lcg64_turning_row_major"),
+                           (0, "3840x2160_lcg64_row_major")):
+            w.set_scene(scene, WIDTH, height)
+            w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+            moving = "turning" in key
+            wall4, k4 = time_frames(w, pipe4, pitch, args.steps, args.warmup, stream,
+                                    per_frame=turn if moving else None)
+            result["also"][key] = {
+                "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall4 / 1e6, 2),
+                "fps": round(args.steps / wall4, 2), "kernel_ms": round(k4, 4),
+                "camera": "rotation = 0.004 rad x frame index" if moving else "static pose (0,0)",
+                "tile_order": "adaptive" if order else "row-major (SFRT_OPT_TILE_ORDER 0)"}
         w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
-        result["also"]["3840x2160_lcg64_row_major"] = {
-            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall5 / 1e6, 2),
-            "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4),
-            "tile_order": "row-major (SFRT_OPT_TILE_ORDER 0)"}
+        w.set_scene(scene, WIDTH, height)
         del pipe4
+        # Beyond the reference's scene sizes: 256 spheres (the n > 64 kernel).
+        w5 = sfrt.World(local_rank)
+        w5.load_texture(*floor)
+        w5.set_scene(scenes.lcg256(), WIDTH, height)
+        pipe5 = BandPipeline(0, 1, height, pitch, "cuda")
+        wall5, k5 = time_frames(w5, pipe5, pitch, args.steps, args.warmup, stream)
+        result["also"]["3840x2160_lcg256"] = {
+            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall5 / 1e6, 2),
+            "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4), "spheres": 256}
+        w5.close()
+        del pipe5
         if not args.no_cpu_baseline:
             torch.cuda.synchronize()
             gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()

@@ -137,14 +137,16 @@ SFRT_API int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count
 
 /* Options: SFRT_OPT_CULL (1 = per-wave sphere culling, default; 0 = visit
  * every sphere -- same bytes, slower; used by A/B parity tests).
- * SFRT_OPT_VARIANT: kernel tuning variant for A/B timing (0 = default build;
- * every variant produces the same bytes).
+ * SFRT_OPT_RAYS_PER_LANE (0 = default): pixels per lane of the <= 64-sphere
+ * kernel, i.e. its (8R)x8 tile width; 1-4 force that kernel (parity tests run
+ * every shipped tile shape through it; same bytes), 0 lets the kernel table
+ * choose (sphere_trace.hip trace_rays).  Ignored above 64 spheres.
  * SFRT_OPT_TILE_ORDER (1 = default): sfrt_world_render_band dispatches the tiles
  * of a frame longest-first by the march steps an earlier render_band of the same
- * geometry recorded (two frames back; the sort runs on a world-owned stream,
- * overlapped); 0 = row-major order.  Scheduling only: same bytes either way. */
+ * geometry recorded (two frames back; the sort runs inside the next launch);
+ * 0 = row-major order.  Scheduling only: same bytes either way. */
 #define SFRT_OPT_CULL 1
-#define SFRT_OPT_VARIANT 2
+#define SFRT_OPT_RAYS_PER_LANE 2
 #define SFRT_OPT_TILE_ORDER 3
 SFRT_API int sfrt_world_set_option(sfrt_world* w, int option, int value);
 
@@ -214,8 +216,7 @@ SFRT_API int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pit
 SFRT_API int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream);
 /* SFRT_OPT_TILE_ORDER as for sfrt_world, but off (0) by default here: render_band with 1
  * dispatches 8x8 tiles longest-first by the DDA + shadow steps of two frames back (same
- * bytes; measured 1-6% slower on the voxel worlds); SFRT_OPT_VARIANT (A/B,
- * same bytes): 1 = the 2-D-grid kernel, 3 = the grid's occupancy bitmask staged in LDS. */
+ * bytes; measured 1-6% slower on the voxel worlds). */
 SFRT_API int sfrt_voxel_set_option(sfrt_voxel* v, int option, int value);
 
 /* ======================================================================
@@ -266,8 +267,7 @@ SFRT_API int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int heigh
 /* rt.draw + rt.getTexture().copyToImage() into a host RGBA8 buffer (synchronous). */
 SFRT_API int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height);
 SFRT_API int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream);
-/* SFRT_OPT_VARIANT: kernel variant for A/B timing (same bytes; tests check it).
- * SFRT_OPT_TILE_ORDER as for sfrt_world, off (0) by default here: sfrt_glsl_draw with 1
+/* SFRT_OPT_TILE_ORDER as for sfrt_world, off (0) by default here: sfrt_glsl_draw with 1
  * dispatches 8x8 tiles longest-first by the metaball-march steps of two frames back (same
  * bytes; measured 20-30% slower on the GLSL frames). */
 SFRT_API int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value);

@@ -53,7 +53,6 @@ struct GlslFrame {
   int32_t sc, lc, all;
   int32_t cam_negzero;                 // a campos component is -0.0 (wall pass, below)
   int32_t wall_start;                  // first wall-pass iteration that can change a lane
-  int32_t variant;                     // tuning A/B (sfrt_glsl_set_option): 1 = records staged in LDS
   int32_t width, height, row0, rows, tiles_x;
   const GlslWall* walls;
   const GlslBall* balls;               // all - sc entries (lights, then ospheres)

@@ -51,7 +51,6 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
   return (uint32_t)(int)floorf(v * 255.0f + 0.5f);
 }
 
-template <bool LDS>
 __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __restrict__ walls,
                                          const GlslBall* __restrict__ balls, int i, int row,
                                          uint32_t& work, bool store = true) {
@@ -246,26 +245,18 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
 }
 
 // Wall and ball records are read once per visit by every wave, with scalar
-// loads (wave-uniform addresses, scalar cache).  Variant 1 stages them in LDS
-// instead (one copy per workgroup); measured slower on MI355X
-// (profiles/r1_glsl_variants.json), kept for A/B.
-template <bool LDS, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) void k_glsl(GlslFrame f) {
-  __shared__ GlslWall s_walls[LDS ? kGlslMax : 1];
-  __shared__ GlslBall s_balls[LDS ? kGlslMax : 1];
-  if (LDS) {
-    for (int t = threadIdx.x; t < f.sc; t += blockDim.x) s_walls[t] = f.walls[t];
-    for (int t = threadIdx.x; t < f.all - f.sc; t += blockDim.x) s_balls[t] = f.balls[t];
-    __syncthreads();
-  }
+// loads (wave-uniform addresses, scalar cache); staging them in LDS measured
+// 5-10% slower (profiles/r1_glsl_variants.json).  Four 8x8 tiles (one per
+// wave) per 256-thread workgroup, row-major.
+__global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
   const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * WPB + (WPB == 1 ? 0 : (int)(threadIdx.x >> 6));
+  const int tile = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   const int tx = tile % f.tiles_x, ty = tile / f.tiles_x;
   const int i = tx * 8 + (lane & 7);
   const int r = ty * 8 + (lane >> 3);
   if (i >= f.width || r >= f.rows) return;
   uint32_t work = 0;
-  fragment<LDS>(f, LDS ? s_walls : f.walls, LDS ? s_balls : f.balls, i, f.row0 + r, work);
+  fragment(f, f.walls, f.balls, i, f.row0 + r, work);
 }
 
 // One 8x8 tile per one-wave workgroup in the adaptive tile order (sfrt_device.h
@@ -293,7 +284,7 @@ __global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
   // branch around fragment() would cost its wave-uniform skips their uniformity.
   const bool in = i < f.width && r < f.rows;
   uint32_t work = 0;
-  fragment<false>(f, f.walls, f.balls, i < f.width ? i : f.width - 1,
+  fragment(f, f.walls, f.balls, i < f.width ? i : f.width - 1,
                   f.row0 + (r < f.rows ? r : f.rows - 1), work, in);
   if (f.tile_cost) {
     const uint32_t w = wave_max_u32(work);  // the tile's longest march
@@ -305,7 +296,7 @@ __global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
 
 long long glsl_tile_key(const GlslFrame& f, long long* tiles) {
   *tiles = 0;
-  if (f.variant != 0 || f.tiles_x <= 0 || f.rows <= 0) return 0;
+  if (f.tiles_x <= 0 || f.rows <= 0) return 0;
   const long long ty = (f.rows + 7) / 8;
   *tiles = (long long)f.tiles_x * ty;
   return (1ll << 62) | ((long long)f.tiles_x << 28) | ty;
@@ -321,13 +312,7 @@ int launch_glsl(const GlslFrame& f, void* stream) {
                        (hipStream_t)stream, f, (int)tiles);
     return hipGetLastError() != hipSuccess;
   }
-  const dim3 g((unsigned)((tiles + 3) / 4)), b(256);
-  if (f.variant == 1)
-    hipLaunchKernelGGL(k_glsl<true>, g, b, 0, (hipStream_t)stream, f);
-  else if (f.variant == 2)  // one wave per workgroup (measured equal to four)
-    hipLaunchKernelGGL((k_glsl<false, 1>), dim3((unsigned)tiles), dim3(64), 0, (hipStream_t)stream, f);
-  else
-    hipLaunchKernelGGL(k_glsl<false>, g, b, 0, (hipStream_t)stream, f);
+  hipLaunchKernelGGL(k_glsl, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, (hipStream_t)stream, f);
   return hipGetLastError() != hipSuccess;
 }
 

@@ -19,29 +19,13 @@
 
 #include "glsl_trace.h"
 #include "sfrt.h"
+#include "sfrt_host.h"
 #include "sfrt_sched.h"
 #include "sfrt_math.h"
 
 #pragma clang fp contract(off)
 
 namespace {
-
-#define HIP_TRY(expr)                            \
-  do {                                           \
-    if ((expr) != hipSuccess) return SFRT_E_HIP; \
-  } while (0)
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
 // Uniform values are bounded so that every product in the wall pass stays
 // finite (the kernel's step-0 shortcut relies on it).
@@ -108,7 +92,6 @@ struct sfrt_glsl {
   int device = 0;
   sfrt_glsl_uniforms u{};
   int ground_w = 0, ground_h = 0;
-  int variant = 0;                     // SFRT_OPT_VARIANT (tuning A/B)
   int tile_order_on = 0;               // SFRT_OPT_TILE_ORDER (sfrt_glsl_draw): off by default, slower here
   sfrt::TileSched sched;               // adaptive tile order (sfrt_sched.h)
   // device resources
@@ -137,7 +120,7 @@ struct sfrt_glsl {
   std::mutex mu;
 
   ~sfrt_glsl() {
-    DeviceGuard g(device);
+    sfrt::DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
     (void)hipDeviceSynchronize();
     sched.release();
@@ -205,7 +188,6 @@ struct sfrt_glsl {
     f.sc = sc;
     f.lc = lc;
     f.all = all;
-    f.variant = variant;
     f.cam_negzero = (std::signbit(v.campos[0]) && v.campos[0] == 0.0f) ||
                     (std::signbit(v.campos[1]) && v.campos[1] == 0.0f) ||
                     (std::signbit(v.campos[2]) && v.campos[2] == 0.0f);
@@ -356,7 +338,7 @@ int sfrt_glsl_create(int hip_device, sfrt_glsl** out) {
     return SFRT_E_HIP;
   sfrt_glsl* g = new sfrt_glsl();
   g->device = hip_device;
-  DeviceGuard dg(hip_device);
+  sfrt::DeviceGuard dg(hip_device);
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&g->d_status, sizeof(int)) != hipSuccess ||
       hipMemset(g->d_status, 0, sizeof(int)) != hipSuccess) {
@@ -375,7 +357,7 @@ int sfrt_glsl_set_ground(sfrt_glsl* g, const uint8_t* rgba, int w, int h) {
   std::vector<uint32_t> chain;
   int lw[sfrt::kGlslMipLevels], lh[sfrt::kGlslMipLevels], off[sfrt::kGlslMipLevels], levels = 0;
   build_mips(rgba, w, h, chain, lw, lh, off, &levels);
-  DeviceGuard dg(g->device);
+  sfrt::DeviceGuard dg(g->device);
   HIP_TRY(hipDeviceSynchronize());  // draws on any stream may still read the old chain
   (void)hipFree(g->d_mip);
   g->d_mip = nullptr;
@@ -447,7 +429,7 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
       height >= (1 << 24) || width >= (1 << 24))
     return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(g->mu);
-  DeviceGuard dg(g->device);
+  sfrt::DeviceGuard dg(g->device);
   hipStream_t s = (hipStream_t)hip_stream;
   sfrt::GlslFrame f;
   if (rows == 0) return SFRT_OK;
@@ -468,8 +450,9 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
   f.tile_cost = p.tile_cost;
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
-  if (sfrt::launch_glsl(f, s)) return SFRT_E_HIP;
-  HIP_TRY(g->sched.end(p, s));
+  const bool queued = sfrt::launch_glsl(f, s) == 0;
+  HIP_TRY(g->sched.end(p, s, queued));
+  if (!queued) return SFRT_E_HIP;
   return g->launched(s);
 }
 
@@ -477,7 +460,7 @@ int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
   if (!g || !pixels || width <= 0 || height <= 0 || height >= (1 << 24) || width >= (1 << 24))
     return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(g->mu);
-  DeviceGuard dg(g->device);
+  sfrt::DeviceGuard dg(g->device);
   const size_t px = (size_t)width * height;
   if (g->d_frame_px < px) {
     HIP_TRY(hipStreamSynchronize(g->stream));
@@ -505,10 +488,6 @@ int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
 int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value) {
   if (!g) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(g->mu);
-  if (option == SFRT_OPT_VARIANT) {
-    g->variant = value;
-    return SFRT_OK;
-  }
   if (option == SFRT_OPT_TILE_ORDER) {
     g->tile_order_on = value == 2 ? 2 : value ? 1 : 0;
     return SFRT_OK;
@@ -519,7 +498,7 @@ int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value) {
 int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream) {
   if (!g) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(g->mu);
-  DeviceGuard dg(g->device);
+  sfrt::DeviceGuard dg(g->device);
   return g->read_status((hipStream_t)hip_stream);
 }
 

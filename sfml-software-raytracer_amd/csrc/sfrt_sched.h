@@ -32,6 +32,8 @@ struct TileSched {
   int64_t k = 0;
   long long key_prev = 0;        // tile grid of launch k-1 (0: none)
   bool sorted_prev = false;      // launch k-1 sorted launch k-2's tiles into order[k % 2]
+  long long pending_key = 0;     // begin() -> end(): the launch being queued
+  bool pending_sorted = false;
   hipStream_t last_stream = nullptr;
   bool have_last = false;
 
@@ -47,23 +49,22 @@ struct TileSched {
 
   // Link a launch on s with tile grid `key` (0: takes no part) of `tiles` tiles
   // into the chain.  mode: 1 = adaptive; 2 = timing probe (reuse the last order,
-  // no sorter, the chain does not advance).
+  // no sorter, the chain does not advance).  The chain state moves only in end(),
+  // once the launch is known to be queued.
   hipError_t begin(long long key, long long tiles, hipStream_t s, int mode, TileSchedPtrs& p) {
     p = TileSchedPtrs{};
+    pending_key = 0;
     if (key == 0 || mode == 0) return hipSuccess;
     hipError_t e;
     if (tiles > cap) {  // (re)allocate; a new chain starts
       if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
       release();
+      reset();
       for (int q = 0; q < 2; q++) {
         if ((e = hipMalloc(&order[q], sizeof(uint32_t) * (size_t)tiles)) != hipSuccess) return e;
         if ((e = hipMalloc(&cost[q], (size_t)tiles)) != hipSuccess) return e;
       }
       cap = tiles;
-      k = 0;
-      key_prev = 0;
-      sorted_prev = false;
-      have_last = false;
     }
     // A launch on another stream than the previous one: the host waits for the
     // previous one (rare; an event recorded after every launch would instead put a
@@ -77,20 +78,38 @@ struct TileSched {
     p.next_order = order[(k + 1) & 1];
     if (mode == 2 && sorted_prev && same) {
       p.prev_cost = nullptr;
-      return hipSuccess;
+      return hipSuccess;  // nothing to commit
     }
-    sorted_prev = same;
-    key_prev = key;
-    k++;
+    pending_key = key;
+    pending_sorted = same;
     return hipSuccess;
   }
 
-  // After the launch that took part (p.tile_cost set) was queued on s.
-  hipError_t end(const TileSchedPtrs& p, hipStream_t s) {
+  // After the launch that took part (p.tile_cost set) was queued on s (queued =
+  // false: it failed).  A failed launch restarts the chain: its cost buffer was
+  // never written, so no later launch may sort it or read an order built from it.
+  hipError_t end(const TileSchedPtrs& p, hipStream_t s, bool queued = true) {
     if (!p.tile_cost) return hipSuccess;
+    if (!queued) {
+      reset();
+      return hipSuccess;
+    }
+    if (pending_key) {
+      sorted_prev = pending_sorted;
+      key_prev = pending_key;
+      k++;
+      pending_key = 0;
+    }
     last_stream = s;
     have_last = true;
     return hipSuccess;
+  }
+
+  void reset() {
+    k = 0;
+    key_prev = 0;
+    sorted_prev = false;
+    pending_key = 0;
   }
 };
 

@@ -49,7 +49,7 @@ struct FrameRec {
   int tiles_x;                      // ceil(sub_w / 8)
   int cull;                         // 1: per-wave cone culling (default), 0: every sphere
   float cull_margin;                // absolute inflation of every sphere in the cone test
-  int variant;                      // kernel variant for tuning A/B (0 = default)
+  int rays;                         // SFRT_OPT_RAYS_PER_LANE: 0 = the kernel table's choice, 1-4 forced
   long long out_pitch;              // output pitch in pixels
   uint32_t* out;                    // pixel (a, b) -> out[(b - sub_row0) * out_pitch + a]
   const uint32_t* tex;              // RGBA8 texture atlas (every loaded slot, back to back)

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "sfrt.h"
+#include "sfrt_host.h"
 #include "sfrt_sched.h"
 #include "sfrt_math.h"
 #include "voxel_trace.h"
@@ -27,23 +28,6 @@
 namespace {
 
 constexpr float kPI = 3.1415926535f;  // World.h:5
-
-#define HIP_TRY(expr)                            \
-  do {                                           \
-    if ((expr) != hipSuccess) return SFRT_E_HIP; \
-  } while (0)
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
 // float -> unsigned as the reference's x86-64 build converts it.
 uint32_t to_u32(float f) {
@@ -90,9 +74,6 @@ struct sfrt_voxel {
   DevTex tex[sfrt::kVoxSlots], dyn_tex[sfrt::kVoxSlots];
   int16_t* d_blocks = nullptr;
   size_t d_blocks_cap = 0;
-  uint32_t* d_occ = nullptr;   // 1 bit per dense cell: non-empty (LDS-staged by the kernel)
-  size_t d_occ_cap = 0;
-  int occ_words = 0;
   bool blocks_dirty = true;
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
@@ -111,13 +92,12 @@ struct sfrt_voxel {
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
-  int variant = 0;           // SFRT_OPT_VARIANT (A/B: 1 = the 2-D grid kernel)
   int tile_order_on = 0;     // SFRT_OPT_TILE_ORDER: off by default here (slower)
   sfrt::TileSched sched;     // adaptive tile order (sfrt_sched.h), render_band
   std::mutex mu;
 
   ~sfrt_voxel() {
-    DeviceGuard g(device);
+    sfrt::DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
     (void)hipDeviceSynchronize();
     sched.release();
@@ -125,7 +105,6 @@ struct sfrt_voxel {
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
     (void)hipFree(d_blocks);
-    (void)hipFree(d_occ);
     for (auto& t : slots) {
       (void)hipFree(t.d);
       (void)hipHostFree(t.h);
@@ -227,27 +206,11 @@ struct sfrt_voxel {
       }
       HIP_TRY(hipMemcpy(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
                         hipMemcpyHostToDevice));
-      // occupancy bitmask of the dense grid, index (x * ny + y) * nz + z
-      const size_t words = (blocks.size() + 31) / 32;
-      std::vector<uint32_t> occ(words, 0u);
-      for (size_t c = 0; c < blocks.size(); c++)
-        if (blocks[c] != sfrt::kVoxEmpty) occ[c >> 5] |= 1u << (c & 31);
-      if (d_occ_cap < words) {
-        (void)hipFree(d_occ);
-        d_occ = nullptr;
-        d_occ_cap = 0;
-        HIP_TRY(hipMalloc(&d_occ, words * sizeof(uint32_t)));
-        d_occ_cap = words;
-      }
-      HIP_TRY(hipMemcpy(d_occ, occ.data(), words * sizeof(uint32_t), hipMemcpyHostToDevice));
-      occ_words = (int)words;
       blocks_dirty = false;
     }
     f.col = (const float*)d;
     f.row = (const float*)(d + b_col);
     f.blocks = d_blocks;
-    f.occ = d_occ;
-    f.occ_words = occ_words;
     f.nx = nx; f.ny = ny; f.nz = nz;
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
       f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};
@@ -293,7 +256,7 @@ int sfrt_voxel_create(int hip_device, sfrt_voxel** out) {
   v->cam.pos[0] = 15.5f; v->cam.pos[1] = 1.9f; v->cam.pos[2] = 15.5f;
   v->cam.fov_h = 75.0f * (kPI / 180.0f);
   v->cam.fov_v = 47.0f * (kPI / 180.0f);
-  DeviceGuard g(hip_device);
+  sfrt::DeviceGuard g(hip_device);
   if (hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&v->d_status, sizeof(int)) != hipSuccess ||
       hipMemset(v->d_status, 0, sizeof(int)) != hipSuccess) {
@@ -353,7 +316,7 @@ int sfrt_voxel_set_blocks(sfrt_voxel* v, const int16_t* texture_ids, int nx, int
 int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h) {
   if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
-  DeviceGuard g(v->device);
+  sfrt::DeviceGuard g(v->device);
   HIP_TRY(hipDeviceSynchronize());  // launches on any stream may read it
   return upload_texture(v->tex[slot], rgba, w, h);
 }
@@ -361,7 +324,7 @@ int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w,
 int sfrt_voxel_load_dyn_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h) {
   if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
-  DeviceGuard g(v->device);
+  sfrt::DeviceGuard g(v->device);
   HIP_TRY(hipDeviceSynchronize());
   return upload_texture(v->dyn_tex[slot], rgba, w, h);
 }
@@ -397,7 +360,7 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   const int sub_h = ystart < v->height ? (v->height - ystart + yadd - 1) / yadd : 0;
   if (v->blocks.empty()) return SFRT_E_EMPTY;
   if (sub_w == 0 || sub_h == 0) return SFRT_OK;
-  DeviceGuard g(v->device);
+  sfrt::DeviceGuard g(v->device);
   const size_t px = (size_t)sub_w * sub_h;
   if (v->d_frame_px < px) {
     (void)hipFree(v->d_frame);
@@ -408,7 +371,6 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   sfrt::VoxFrame f;
   int rc = v->prepare(f, v->stream);
   if (rc) return rc;
-  f.variant = v->variant;
   f.xstart = xstart; f.xadd = xadd; f.ystart = ystart; f.yadd = yadd;
   f.sub_w = sub_w;
   f.sub_row0 = 0;
@@ -436,7 +398,7 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   std::lock_guard<std::mutex> lk(v->mu);
   if (pitch_bytes < (int64_t)v->width * 4 || row0 + rows > v->height) return SFRT_E_INVALID;
   if (rows == 0) return SFRT_OK;
-  DeviceGuard g(v->device);
+  sfrt::DeviceGuard g(v->device);
   hipStream_t s = (hipStream_t)hip_stream;
   sfrt::VoxFrame f;
   int rc = v->prepare(f, s);
@@ -447,7 +409,6 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   f.sub_rows = rows;
   f.out = (uint32_t*)dev_pixels;
   f.out_pitch = pitch_bytes / 4;
-  f.variant = v->variant;
   long long tiles = 0;
   const long long key = v->tile_order_on ? sfrt::voxel_tile_key(f, &tiles) : 0;
   sfrt::TileSchedPtrs p;
@@ -456,18 +417,15 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   f.tile_cost = p.tile_cost;
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
-  if (sfrt::launch_voxel(f, s)) return SFRT_E_HIP;
-  HIP_TRY(v->sched.end(p, s));
+  const bool queued = sfrt::launch_voxel(f, s) == 0;
+  HIP_TRY(v->sched.end(p, s, queued));
+  if (!queued) return SFRT_E_HIP;
   return v->launched(s);
 }
 
 int sfrt_voxel_set_option(sfrt_voxel* v, int option, int value) {
   if (!v) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
-  if (option == SFRT_OPT_VARIANT) {
-    v->variant = value;
-    return SFRT_OK;
-  }
   if (option == SFRT_OPT_TILE_ORDER) {
     v->tile_order_on = value == 2 ? 2 : value ? 1 : 0;
     return SFRT_OK;
@@ -478,7 +436,7 @@ int sfrt_voxel_set_option(sfrt_voxel* v, int option, int value) {
 int sfrt_voxel_check(sfrt_voxel* v, void* hip_stream) {
   if (!v) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
-  DeviceGuard g(v->device);
+  sfrt::DeviceGuard g(v->device);
   return v->read_status((hipStream_t)hip_stream);
 }
 

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "sfrt.h"
+#include "sfrt_host.h"
 #include "sfrt_math.h"
 #include "sfrt_sched.h"
 #include "sfrt_trace.h"
@@ -102,23 +103,6 @@ float pass_threshold(float r) {
   return t;
 }
 
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-
-#define HIP_TRY(expr)                          \
-  do {                                         \
-    if ((expr) != hipSuccess) return SFRT_E_HIP; \
-  } while (0)
-
 }  // namespace
 
 struct sfrt_world {
@@ -136,7 +120,7 @@ struct sfrt_world {
   int tex_h[SFRT_TEXTURE_SLOTS] = {};
   uint32_t tex_off[SFRT_TEXTURE_SLOTS] = {};  // texel offset of each slot in the atlas
   int cull = 1;
-  int variant = 0;
+  int rays = 0;           // SFRT_OPT_RAYS_PER_LANE (0 = automatic)
   int tile_order_on = 1;  // SFRT_OPT_TILE_ORDER
   // --- device resources ---
   hipStream_t stream = nullptr;
@@ -173,10 +157,10 @@ struct sfrt_world {
   PipeSlot pipe[kPipe];
   hipStream_t copy_stream = nullptr;
   int64_t next_ticket = 0;
-  std::mutex mu;
+  mutable std::mutex mu;  // every entry point, getters included (RenderThreads call concurrently)
 
   ~sfrt_world() {
-    DeviceGuard g(device);
+    sfrt::DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy_stream) (void)hipStreamSynchronize(copy_stream);
     for (PipeSlot& p : pipe) {
@@ -248,7 +232,7 @@ struct sfrt_world {
     f.width = width;
     f.height = height;
     f.cull = cull;
-    f.variant = variant;
+    f.rays = rays;
     // Culling margin (sphere_trace.hip, cull_mask).  A march step
     // pos += dir * L rounds twice per component, so each step moves the
     // position off the ray's exact line by at most ~2.1e-7 * (|pos| + L) <=
@@ -351,11 +335,12 @@ struct sfrt_world {
     return SFRT_OK;
   }
 
-  int sched_end(const sfrt::FrameRec& f, hipStream_t s) {
+  // After launch_trace for f returned (queued = false: it failed).
+  int sched_end(const sfrt::FrameRec& f, hipStream_t s, bool queued) {
     sfrt::TileSchedPtrs p;
     p.tile_cost = f.tile_cost;
-    HIP_TRY(sched.end(p, s));
-    return SFRT_OK;
+    HIP_TRY(sched.end(p, s, queued));
+    return queued ? SFRT_OK : SFRT_E_HIP;
   }
 
   int read_status(hipStream_t s) {
@@ -382,7 +367,7 @@ int sfrt_world_create(int hip_device, sfrt_world** out) {
   // Camera defaults (SphereWorld.h:10-21) and the constructor's conversion (:72-73).
   w->cam.fov_h = sfrt_deg_to_rad(75.0f);
   w->cam.fov_v = sfrt_deg_to_rad(47.0f);
-  DeviceGuard g(hip_device);
+  sfrt::DeviceGuard g(hip_device);
   if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&w->d_status, sizeof(int)) != hipSuccess ||
       hipMemset(w->d_status, 0, sizeof(int)) != hipSuccess) {
@@ -405,6 +390,7 @@ int sfrt_world_set_size(sfrt_world* w, int width, int height) {
 
 int sfrt_world_get_size(const sfrt_world* w, int* width, int* height) {
   if (!w || !width || !height) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
   *width = w->width;
   *height = w->height;
   return SFRT_OK;
@@ -421,6 +407,7 @@ int sfrt_world_set_camera(sfrt_world* w, const sfrt_camera* cam) {
 
 int sfrt_world_get_camera(const sfrt_world* w, sfrt_camera* cam) {
   if (!w || !cam) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
   *cam = w->cam;
   return SFRT_OK;
 }
@@ -442,7 +429,7 @@ int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int te
     total += (size_t)w->tex_w[k] * w->tex_h[k];
   }
   if (total > 0xffffffffull) return SFRT_E_INVALID;
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   HIP_TRY(hipDeviceSynchronize());
   if (w->d_tex_texels < total) {
     (void)hipFree(w->d_tex);
@@ -516,6 +503,7 @@ int sfrt_world_get_sphere_textures(sfrt_world* w, int32_t* out, int capacity, in
 
 int sfrt_world_get_spheres(const sfrt_world* w, sfrt_sphere* out, int capacity, int* count) {
   if (!w || !count) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
   *count = (int)w->spheres.size();
   if (out) {
     const int n = capacity < *count ? capacity : *count;
@@ -538,8 +526,9 @@ int sfrt_world_set_option(sfrt_world* w, int option, int value) {
     w->cull = value ? 1 : 0;
     return SFRT_OK;
   }
-  if (option == SFRT_OPT_VARIANT) {
-    w->variant = value;
+  if (option == SFRT_OPT_RAYS_PER_LANE) {
+    if (value < 0 || value > 4) return SFRT_E_INVALID;
+    w->rays = value;
     return SFRT_OK;
   }
   if (option == SFRT_OPT_TILE_ORDER) {
@@ -559,7 +548,7 @@ int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart, int yadd
   const int sub_w = xstart < w->width ? (w->width - xstart + xadd - 1) / xadd : 0;
   const int sub_h = ystart < w->height ? (w->height - ystart + yadd - 1) / yadd : 0;
   if (sub_w == 0 || sub_h == 0) return SFRT_OK;
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   const size_t px = (size_t)sub_w * sub_h;
   if (w->d_frame_px < px) {
     (void)hipFree(w->d_frame);
@@ -614,7 +603,7 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   if (rc) return rc;
   if (pitch_bytes < (int64_t)w->width * 4 || row0 + rows > w->height) return SFRT_E_INVALID;
   if (rows == 0) return SFRT_OK;
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   hipStream_t s = (hipStream_t)hip_stream;  // HIP convention: NULL = the null stream
   sfrt::FrameRec f;
   std::vector<sfrt::SphereRec> recs;
@@ -629,15 +618,14 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   rc = w->stage_spheres(f, recs, s, false);
   if (rc) return rc;
   if ((rc = w->sched_begin(f, s))) return rc;
-  if (sfrt::launch_trace(f, recs.data(), s)) return SFRT_E_HIP;
-  if ((rc = w->sched_end(f, s))) return rc;
+  if ((rc = w->sched_end(f, s, sfrt::launch_trace(f, recs.data(), s) == 0))) return rc;
   return w->launched(s);
 }
 
 int sfrt_world_check(sfrt_world* w, void* hip_stream) {
   if (!w) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(w->mu);
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   return w->read_status((hipStream_t)hip_stream);
 }
 
@@ -651,7 +639,7 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
       return SFRT_E_INVALID;
   if (count == 0) return SFRT_OK;
   static_assert(sizeof(sfrt_pixel_dump) == sizeof(sfrt::PixelDump), "dump layout");
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   sfrt::FrameRec f;
   std::vector<sfrt::SphereRec> recs;
   w->prepare(f, recs);
@@ -695,7 +683,7 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
   std::lock_guard<std::mutex> lk(w->mu);
   int rc = w->validate();
   if (rc) return rc;
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   if (!w->copy_stream && hipStreamCreateWithFlags(&w->copy_stream, hipStreamNonBlocking) != hipSuccess)
     return SFRT_E_HIP;
   const int64_t t = w->next_ticket;
@@ -731,8 +719,8 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
   if ((rc = w->sched_begin(f, w->stream))) return rc;  // adaptive tile order, as render_band
-  if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
-  if ((rc = w->sched_end(f, w->stream))) return rc;
+  if ((rc = w->sched_end(f, w->stream, sfrt::launch_trace(f, recs.data(), w->stream) == 0)))
+    return rc;
   if ((rc = w->launched(w->stream))) return rc;
   HIP_TRY(hipEventRecord(slot.rendered, w->stream));
   HIP_TRY(hipStreamWaitEvent(w->copy_stream, slot.rendered, 0));
@@ -759,7 +747,7 @@ int sfrt_world_wait_frame(sfrt_world* w, int64_t ticket) {
     ev = slot.copied;
     h_status = slot.h_status;
   }
-  DeviceGuard g(w->device);
+  sfrt::DeviceGuard g(w->device);
   HIP_TRY(hipEventSynchronize(ev));
   const int st = *h_status;
   if (st & 1) return SFRT_E_MARCH_LIMIT;

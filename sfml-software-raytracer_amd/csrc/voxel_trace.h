@@ -47,8 +47,6 @@ struct VoxFrame {
   const float* col;                         // per column i: dir.x, dir.z, atan2f(dir.z, dir.x)
   const float* row;                         // per row j: dir.y, yscale
   const int16_t* blocks;                    // dense [nx][ny][nz], textureID or kVoxEmpty
-  const uint32_t* occ;                      // 1 bit per cell of blocks: non-empty
-  int32_t occ_words;
   int32_t nx, ny, nz;
   VoxTex tex[kVoxSlots];
   VoxTex dyn_tex[kVoxSlots];
@@ -60,8 +58,6 @@ struct VoxFrame {
   long long out_pitch;
   uint32_t* out;
   int* status;                              // bit 1: out-of-range texel read
-  int32_t variant;                          // A/B only: 1 = the 2-D grid, no tile order;
-                                            // 3 = occupancy bitmask in LDS (slower)
   // Adaptive tile order (sfrt_sched.h): one 8x8 tile per one-wave
   // workgroup, slot -> tile_order; cost = the tile's DDA + shadow-ray steps.
   const uint32_t* tile_order;

@@ -40,17 +40,14 @@ struct V3 {
 
 // blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff
 // the key is non-negative and decodes to an occupied cell of the dense grid.
-// With `occ` (the grid's occupancy bitmask staged in LDS), an empty cell -- most
-// DDA steps -- costs one LDS read instead of a dependent global load; the
-// texture id is fetched from global memory only for an occupied cell.
-__device__ __forceinline__ int16_t block_at(const VoxFrame& f, const uint32_t* occ, int32_t x,
-                                            int32_t y, int32_t z) {
+// (Staging a one-bit occupancy map of the grid in LDS measured 7-9% slower:
+// these loads hit the caches)
+__device__ __forceinline__ int16_t block_at(const VoxFrame& f, int32_t x, int32_t y, int32_t z) {
   const int32_t key = (int32_t)(((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z);
   if (key < 0) return kVoxEmpty;
   const int32_t cx = key >> 20, cy = (key >> 10) & 1023, cz = key & 1023;
   if (cx >= f.nx || cy >= f.ny || cz >= f.nz) return kVoxEmpty;
   const long long c = ((long long)cx * f.ny + cy) * f.nz + cz;
-  if (occ && !((occ[c >> 5] >> (c & 31)) & 1u)) return kVoxEmpty;
   return f.blocks[c];
 }
 
@@ -81,7 +78,7 @@ __device__ __forceinline__ uint32_t pack(uint32_t r, uint32_t g, uint32_t b, uin
 
 // World::LRaycast, World.cpp:455-491.
 template <bool RECIP>
-__device__ bool lraycast_t(const VoxFrame& f, const uint32_t* occ, V3 pos, V3 dir, float maxDist,
+__device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
                            uint32_t& work) {
   float dist = 0.0f;
   int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
@@ -96,7 +93,7 @@ __device__ bool lraycast_t(const VoxFrame& f, const uint32_t* occ, V3 pos, V3 di
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
     work++;
-    if (block_at(f, occ, pix, piy, piz) != kVoxEmpty) return false;
+    if (block_at(f, pix, piy, piz) != kVoxEmpty) return false;
     const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
     const float c = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
@@ -113,16 +110,16 @@ __device__ bool lraycast_t(const VoxFrame& f, const uint32_t* occ, V3 pos, V3 di
   return dist >= maxDist;
 }
 
-__device__ bool lraycast(const VoxFrame& f, const uint32_t* occ, V3 pos, V3 dir, float maxDist,
+__device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
                          uint32_t& work) {
   const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
-  if (__builtin_amdgcn_ballot_w64(!ok)) return lraycast_t<false>(f, occ, pos, dir, maxDist, work);
-  return lraycast_t<true>(f, occ, pos, dir, maxDist, work);
+  if (__builtin_amdgcn_ballot_w64(!ok)) return lraycast_t<false>(f, pos, dir, maxDist, work);
+  return lraycast_t<true>(f, pos, dir, maxDist, work);
 }
 
 // World::Raycast, World.cpp:302-453.
 template <bool RECIP>
-__device__ uint32_t raycast_t(const VoxFrame& f, const uint32_t* occ, V3 dir, float yscale,
+__device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
                               float atan_dir, uint32_t& work) {
   const V3 cam{f.cam[0], f.cam[1], f.cam[2]};
   float dist = 0.0f;
@@ -200,7 +197,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, const uint32_t* occ, V3 dir, fl
     dist = tryDist;
     pos = tryPos;
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
-    const int16_t id = block_at(f, occ, pix, piy, piz);
+    const int16_t id = block_at(f, pix, piy, piz);
     if (id != kVoxEmpty) {  // hit a block (World.cpp:385)
       uint32_t c;
       if (id < 0) {
@@ -241,7 +238,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, const uint32_t* occ, V3 dir, fl
             if (L.shadows && tryDist < f.shadow_distance) {
               dd = __builtin_sqrtf(nx * nx + ny * ny + nz * nz);  // VLength
               nx = nx / dd; ny = ny / dd; nz = nz / dd;
-              lit = lraycast(f, occ, pos, V3{nx, ny, nz}, dd, work);
+              lit = lraycast(f, pos, V3{nx, ny, nz}, dd, work);
             }
             if (lit) {
               litr += add * L.r;
@@ -259,32 +256,15 @@ __device__ uint32_t raycast_t(const VoxFrame& f, const uint32_t* occ, V3 dir, fl
   return pack(0, 0, 0, 255);  // sf::Color::Black
 }
 
-__device__ uint32_t raycast(const VoxFrame& f, const uint32_t* occ, V3 dir, float yscale,
+__device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
                             float atan_dir, uint32_t& work) {
   const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
-  if (__builtin_amdgcn_ballot_w64(!ok)) return raycast_t<false>(f, occ, dir, yscale, atan_dir, work);
-  return raycast_t<true>(f, occ, dir, yscale, atan_dir, work);
+  if (__builtin_amdgcn_ballot_w64(!ok)) return raycast_t<false>(f, dir, yscale, atan_dir, work);
+  return raycast_t<true>(f, dir, yscale, atan_dir, work);
 }
 
 // 8x8 pixels per one-wave workgroup (a finished wave's slot refills at once;
-// 0.7-1.5% faster than 16x16 per 256 threads, which -DSFRT_VOXEL_TILE16 restores).
-#ifdef SFRT_VOXEL_TILE16
-constexpr int kVoxTile = 16;
-#else
-constexpr int kVoxTile = 8;
-#endif
-__global__ __launch_bounds__(kVoxTile * kVoxTile) void k_voxel(VoxFrame f) {
-  const int a = blockIdx.x * kVoxTile + (threadIdx.x % kVoxTile);
-  const int b = f.sub_row0 + blockIdx.y * kVoxTile + (threadIdx.x / kVoxTile);
-  if (a >= f.sub_w || b >= f.sub_row0 + f.sub_rows) return;
-  const int i = f.xstart + a * f.xadd;
-  const int j = f.ystart + b * f.yadd;
-  const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
-  uint32_t work = 0;
-  const uint32_t rgba = raycast(f, nullptr, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
-  f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
-}
-
+// 0.7-1.5% faster than 16x16 per 256 threads).
 // The default: 8x8 tiles on a 1-D grid of one-wave workgroups in the adaptive
 // tile order (sfrt_device.h sort_tiles; workgroup 0 is the sorter when
 // prev_cost is set).
@@ -315,7 +295,7 @@ __global__ __launch_bounds__(64) void k_voxel_ordered(VoxFrame f, int tiles_x, i
   const int i = f.xstart + ac * f.xadd;
   const int j = f.ystart + bc * f.yadd;
   const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
-  const uint32_t rgba = raycast(f, nullptr, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
+  const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
   if (in) f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
   if (f.tile_cost) {
     // the tile's slowest ray, in DDA + shadow steps / 4 (the classes' scale)
@@ -326,60 +306,21 @@ __global__ __launch_bounds__(64) void k_voxel_ordered(VoxFrame f, int tiles_x, i
 
 }  // namespace
 
-// A/B (SFRT_OPT_VARIANT 3): four 8x8 tiles (one per wave) per 256-thread
-// workgroup with the grid's occupancy bitmask staged in the workgroup's LDS, so
-// an empty cell costs an LDS read instead of a global load.  Measured 7-9%
-// slower than the default (global lookups hit the caches).
-__global__ __launch_bounds__(256) void k_voxel_occ(VoxFrame f, int tiles_x, int ntiles) {
-  extern __shared__ uint32_t s_occ[];
-  for (int w = threadIdx.x; w < f.occ_words; w += blockDim.x) s_occ[w] = f.occ[w];
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  if (tile >= ntiles) return;  // uniform per wave
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int a = tx * 8 + (lane & 7);
-  const int b = f.sub_row0 + ty * 8 + (lane >> 3);
-  const bool in = a < f.sub_w && b < f.sub_row0 + f.sub_rows;
-  const int ac = a < f.sub_w ? a : f.sub_w - 1;
-  const int bc = b < f.sub_row0 + f.sub_rows ? b : f.sub_row0 + f.sub_rows - 1;
-  uint32_t work = 0;
-  const int i = f.xstart + ac * f.xadd;
-  const int j = f.ystart + bc * f.yadd;
-  const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
-  const uint32_t rgba = raycast(f, s_occ, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
-  if (in) f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
-}
-
-constexpr int kVoxOccMaxBytes = 40 * 1024;  // above this the LDS copy would cost occupancy
-
 long long voxel_tile_key(const VoxFrame& f, long long* tiles) {
   *tiles = 0;
-  if (f.variant == 1 || kVoxTile != 8 || f.sub_w <= 0 || f.sub_rows <= 0) return 0;
+  if (f.sub_w <= 0 || f.sub_rows <= 0) return 0;
   const long long tx = (f.sub_w + 7) / 8, ty = (f.sub_rows + 7) / 8;
   *tiles = tx * ty;
   return (1ll << 62) | (tx << 28) | ty;
 }
 
 int launch_voxel(const VoxFrame& f, void* stream) {
-  if (f.sub_w <= 0 || f.sub_rows <= 0) return 0;
   long long tiles = 0;
-  if (voxel_tile_key(f, &tiles) == 0) {  // A/B: the 2-D grid
-    const dim3 grid((unsigned)((f.sub_w + kVoxTile - 1) / kVoxTile),
-                    (unsigned)((f.sub_rows + kVoxTile - 1) / kVoxTile));
-    hipLaunchKernelGGL(k_voxel, grid, dim3(kVoxTile * kVoxTile), 0, (hipStream_t)stream, f);
-  } else {
-    if (tiles > 0x7ffffffeLL) return -1;
-    const int tiles_x = (f.sub_w + 7) / 8;  // default: k_voxel_ordered (row-major unless ordered)
-    const size_t occ_bytes = (size_t)f.occ_words * 4;
-    if (!f.tile_cost && f.variant == 3 && f.occ && occ_bytes <= (size_t)kVoxOccMaxBytes) {
-      hipLaunchKernelGGL(k_voxel_occ, dim3((unsigned)((tiles + 3) / 4)), dim3(256), occ_bytes,
-                         (hipStream_t)stream, f, tiles_x, (int)tiles);
-    } else {
-      hipLaunchKernelGGL(k_voxel_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64),
-                         0, (hipStream_t)stream, f, tiles_x, (int)tiles);
-    }
-  }
+  if (voxel_tile_key(f, &tiles) == 0) return 0;
+  if (tiles > 0x7ffffffeLL) return -1;
+  // row-major unless the host linked this launch into its tile-order chain
+  hipLaunchKernelGGL(k_voxel_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,
+                     (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -113,7 +113,14 @@ def lcg64() -> Scene:
     return Scene("lcg64", sort_spheres(lcg_spheres()))
 
 
-SCENES = {"one_sphere": one_sphere, "default10": default10, "lcg64": lcg64}
+def lcg256() -> Scene:
+    """Beyond the reference's scenes (11 spheres, SphereWorld.cpp:59-62; AddSphere grows the
+    list, :177-190): {0,0,0,4} + 255 spheres of the same LCG stream as lcg64 (its first 63
+    are lcg64's), sorted.  Exercises the n > 64 kernel."""
+    return Scene("lcg256", sort_spheres(lcg_spheres(count=255)))
+
+
+SCENES = {"one_sphere": one_sphere, "default10": default10, "lcg64": lcg64, "lcg256": lcg256}
 
 
 def load_floor() -> tuple[np.ndarray, int, int]:

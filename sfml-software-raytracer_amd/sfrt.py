@@ -16,10 +16,11 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsfrt.so")
+# SFRT_LIB: another build of the same library (build-flag A/B timing in tools/ only).
+LIB_PATH = os.environ.get("SFRT_LIB") or os.path.join(HERE, "libsfrt.so")
 
 SFRT_OPT_CULL = 1
-SFRT_OPT_VARIANT = 2
+SFRT_OPT_RAYS_PER_LANE = 2
 SFRT_OPT_TILE_ORDER = 3
 ERRORS = {
     0: "SFRT_OK", -1: "SFRT_E_INVALID", -2: "SFRT_E_EMPTY", -3: "SFRT_E_NO_TEXTURE",

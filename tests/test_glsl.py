@@ -171,22 +171,6 @@ def test_gpu_matches_oracle(shader, floor, case):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1])
-def test_gpu_kernel_variants_identical(shader, floor, variant):
-    """Tuning variants (SFRT_OPT_VARIANT) produce the default kernel's bytes."""
-    import sfrt
-    for w, h, u in [(1920, 1080, gs.default_uniforms(1920, 1080, 0.9, 0.1, frames=77)),
-                    (640, 360, gs.random_uniforms(3, 40, 4, 50, 640, 360))]:
-        a = draw(shader, u, w, h)
-        shader.set_option(sfrt.SFRT_OPT_VARIANT, variant)
-        try:
-            b = draw(shader, u, w, h)
-        finally:
-            shader.set_option(sfrt.SFRT_OPT_VARIANT, 0)
-        assert np.array_equal(a, b), first_diff(b, a, w)
-
-
-@pytest.mark.gpu
 def test_gpu_synthetic_ground_mips(shader, floor):
     """Non-square ground (64x32: 2x1 box levels) over the default uniforms."""
     import sfrt

@@ -95,32 +95,46 @@ def test_cull_on_off_identical(world, floor):
     assert diff_report(a, b, 3840) == ""
 
 
-@pytest.mark.parametrize("variant", [1, 2, 6, 8, 16, 17, 32, 35, 36, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 52,
-                                     61, 62, 63, 64, 67, 71, 72, 73, 74, 75, 80, 81, 82, 83, 84, 85, 86, 94, 95, 96, 97])
-def test_kernel_variants_identical(world, floor, variant):
-    """Tuning variants (SFRT_OPT_VARIANT: SGPR slot count, LDS-backed sphere list)
-    produce the default kernel's bytes (64 spheres, 4K, rotated pose)."""
+@pytest.mark.parametrize("rays", [1, 2, 3, 4])
+def test_tile_shapes_identical(world, floor, rays):
+    """Every shipped tile shape of the <= 64-sphere kernel ((8R)x8 tiles, R pixels per lane,
+    forced with SFRT_OPT_RAYS_PER_LANE) produces the default kernel's bytes, in row-major
+    order (update_image) and in the adaptive tile order (three render_band frames back to
+    back), on ragged frames (64 spheres, 4K, rotated pose; random poses of three scenes)."""
     import sfrt
+    import torch
     cases = [(scenes.lcg64(), (1.1, -0.2), 3840, 2160)]
-    rng = np.random.default_rng(variant)
+    rng = np.random.default_rng(rays)
     for sc in (scenes.lcg64(), scenes.default10(), scenes.one_sphere()):
         for _ in range(4):
             cases.append((sc, (float(rng.uniform(0, 6.3)), float(rng.uniform(-0.6, 0.6))), 1000, 563))
+    stream = torch.cuda.Stream()
     for sc, pose, width, height in cases:
         world.set_scene(sc.posed(*pose), width, height)
         a = world.render()
-        world.set_option(sfrt.SFRT_OPT_VARIANT, variant)
+        world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
         try:
             b = world.render()
+            assert diff_report(a, b, width) == "", (sc.name, pose, "row-major")
+            bufs = []
+            for _ in range(3):
+                buf = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                torch.cuda.synchronize()
+                world.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+                bufs.append(buf)
+            world.check(stream.cuda_stream)
+            torch.cuda.synchronize()
         finally:
-            world.set_option(sfrt.SFRT_OPT_VARIANT, 0)
-        assert diff_report(a, b, width) == "", (sc.name, pose)
+            world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
+        for k, buf in enumerate(bufs):
+            assert diff_report(buf.cpu().numpy().ravel(), a, width) == "", (sc.name, pose, "ordered", k)
 
 
 @pytest.mark.parametrize("count", [65, 120, 199, 1023])
-def test_global_window_matches_word_lists(world, floor, count):
-    """n > 64: the windowed kernel equals the per-word culled-list kernel
-    (variant 2) for several poses, and the oracle for one of them."""
+def test_global_window_cull_on_off(world, floor, count):
+    """n > 64 (8x8 tiles, multi-word culling masks, march windows in LDS): culling and the
+    window on equal culling off (every sphere every step) for several poses, and the oracle
+    for one of them."""
     import sfrt
     spheres = scenes.sort_spheres(scenes.lcg_spheres(count=count - 1, seed=31 + count))
     rng = np.random.default_rng(count)
@@ -129,11 +143,11 @@ def test_global_window_matches_word_lists(world, floor, count):
         scene = scenes.Scene("many", spheres).posed(*pose)
         world.set_scene(scene, 1000, 563)
         a = world.render()
-        world.set_option(sfrt.SFRT_OPT_VARIANT, 2)
+        world.set_option(sfrt.SFRT_OPT_CULL, 0)
         try:
             b = world.render()
         finally:
-            world.set_option(sfrt.SFRT_OPT_VARIANT, 0)
+            world.set_option(sfrt.SFRT_OPT_CULL, 1)
         assert diff_report(a, b, 1000) == "", (count, pose)
         if q == 0 and count <= 200:
             want = oracle_for(scene, 1000, 563, floor).render(host_threads())
@@ -314,31 +328,33 @@ def test_cpp_host_api(built, tmp_path):
     assert r.returncode == 0 and "failures=0" in r.stdout, r.stdout + r.stderr
 
 
-def test_pipelined_frames_match_update_image(world, floor):
-    """Display path: two frames in flight, camera changing per frame."""
+def test_pipelined_frames_match_oracle(world, floor):
+    """Display path (the reference uploads the filled frame with
+    screenTexture.loadFromImage, Source.cpp:141): two frames in flight through
+    submit_frame / wait_frame into pinned host frames, the camera changing every frame.
+    Each delivered frame equals the oracle's frame of its own pose, byte for byte."""
     import sfrt
     width, height = 640, 360
     scene = scenes.lcg64()
     poses = [(0.1 * k, 0.05 * (k % 3) - 0.05) for k in range(6)]
+    want = {p: oracle_for(scene.posed(*p), width, height, floor).render(host_threads()) for p in poses}
     frames = [sfrt.HostFrame(width * height * 4) for _ in range(3)]
     world.set_scene(scene, width, height)
     tickets = []
-    for k, pose in enumerate(poses):
-        world.set_camera(scene.cam_pos, *pose)
-        tickets.append((world.submit_frame(frames[k % 3]), k))
-        if k >= 1:  # keep at most two frames in flight, check the older one
-            t, kk = tickets.pop(0)
+    try:
+        for k, pose in enumerate(poses):
+            world.set_camera(scene.cam_pos, *pose)
+            tickets.append((world.submit_frame(frames[k % 3]), k))
+            if k >= 1:  # keep at most two frames in flight, check the older one
+                t, kk = tickets.pop(0)
+                world.wait_frame(t)
+                assert diff_report(frames[kk % 3].array, want[poses[kk]], width) == "", kk
+        for t, kk in tickets:
             world.wait_frame(t)
-            world.set_camera(scene.cam_pos, *poses[kk])
-            want = world.render()
-            world.set_camera(scene.cam_pos, *poses[k])
-            assert diff_report(frames[kk % 3].array, want, width) == "", kk
-    for t, kk in tickets:
-        world.wait_frame(t)
-        world.set_camera(scene.cam_pos, *poses[kk])
-        assert diff_report(frames[kk % 3].array, world.render(), width) == "", kk
-    for fr in frames:
-        fr.free()
+            assert diff_report(frames[kk % 3].array, want[poses[kk]], width) == "", kk
+    finally:
+        for fr in frames:
+            fr.free()
 
 
 def _fuzz_scene(seed):
@@ -481,13 +497,14 @@ def test_adaptive_tile_order_4k_frames(world, floor):
         assert torch.equal(b, rowmajor[p]), (k, p)
 
 
-def test_adaptive_order_ragged_24x8_tiles(world, floor):
-    """A large ragged frame (3333 x 2111: >= 32768 tiles of 24x8, three pixels per lane, edge
-    lanes in both directions) through the ordered render_band path, four frames back to back
-    with two poses: every frame equals update_image's (the row-major 16x8 kernel) bytes, and
-    one of them the oracle's."""
+@pytest.mark.parametrize("width,height", [(3333, 2111), (3900, 2170)])
+def test_adaptive_order_ragged_wide_tiles(world, floor, width, height):
+    """Large ragged frames through the ordered render_band path: 3333 x 2111 picks 24x8 tiles
+    (27,720 tiles of 32x8 < 30,000 <= 36,696 of 24x8), 3900 x 2170 picks 32x8 tiles (33,184;
+    3900 % 32 = 28 and 2170 % 8 = 2, so edge lanes in both directions).  Four frames back to
+    back with two poses: every frame equals update_image's (the row-major 16x8 kernel) bytes,
+    and one of them the oracle's."""
     import torch
-    width, height = 3333, 2111
     poses = [(0.4, 0.1), (2.0, -0.3)]
     want = {}
     for p in poses:

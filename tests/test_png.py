@@ -4,10 +4,13 @@ reproduces sf::Image::loadFromFile -> stb_image's 4-channel output.
 PNGs written by the encoder below -- every colour type and bit depth, tRNS,
 Adam7, all five filters, split IDAT, ancillary chunks -- must decode to the
 pixels they were built from, expanded by stb_image's rules; a PIL-written
-PNG must decode like PIL reads it.  Host-only (no GPU).  The reference's own
-PNG files are not used (copying them in was refused).
+PNG must decode like PIL reads it.  Host-only (no GPU).  In the build
+container, the reference's own six PNGs (read in place, never copied) must
+decode to the committed assets byte for byte (test_reference_pngs_decode_to_assets);
+on the GPU box, which has no /root/reference, that test skips.
 """
 import io
+import os
 import struct
 import zlib
 
@@ -31,6 +34,29 @@ def test_pil_written_png(sfrt):
         rgba, w, h = sfrt.decode_png(buf.getvalue())
         assert (w, h) == img.size
         assert np.array_equal(rgba, np.asarray(img.convert("RGBA")).ravel())
+
+
+REF_DIR = "/root/reference/Raytracing"
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                      "sfml-software-raytracer_amd", "assets")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DIR), reason="reference checkout absent (GPU box)")
+@pytest.mark.parametrize("name", ["Floor", "Wall", "Ceiling", "Block", "dynamic", "Projectile"])
+def test_reference_pngs_decode_to_assets(sfrt, name):
+    """The product decoder on the reference's textures (SphereWorld.cpp:52 loads Floor.png, the
+    only texel source of the sphere path, :376-377; World.cpp:40-45 the others) gives exactly
+    the committed RGBA8 assets the renderers and the oracles load."""
+    with open(os.path.join(REF_DIR, f"{name}.png"), "rb") as f:
+        rgba, w, h = sfrt.decode_png(f.read())
+    with open(os.path.join(ASSETS, f"{name}.rgba.shape")) as f:
+        want_w, want_h = (int(v) for v in f.read().split())
+    want = np.fromfile(os.path.join(ASSETS, f"{name}.rgba"), dtype=np.uint8)
+    assert (w, h) == (want_w, want_h)
+    assert np.array_equal(rgba, want)
+    if name == "Floor":
+        floor = np.fromfile(os.path.join(ASSETS, "floor_128x128.rgba"), dtype=np.uint8)
+        assert np.array_equal(rgba, floor)
 
 
 # ---------- a small PNG encoder for synthetic cases ----------

@@ -118,7 +118,7 @@ def test_voxel_gpu_subsets_and_bands(vworld, assets):
 def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
     """SFRT_OPT_TILE_ORDER on the voxel renderer: frames rendered back to back through
     render_band (order from two frames back, poses and sizes changing, a row band) equal
-    the row-major 2-D-grid kernel's frames (SFRT_OPT_VARIANT 1) and the oracle."""
+    the row-major frames of update_image and the oracle."""
     import sfrt
     import torch
     seq = [((15.5, 1.9, 15.5), 0.0, 0.0, 640, 360, 0, 360)] * 4 + \
@@ -128,45 +128,24 @@ def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
     stream = torch.cuda.Stream()
     frames = []
     vworld.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)  # off by default for the voxel renderer
-    with torch.cuda.stream(stream):
-        for p, r, hr, width, height, r0, rows in seq:
-            vworld.set_scene(vs.default_world(p, r, hr), width, height)
-            b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
-            vworld.render_band(b[r0].data_ptr(), width * 4, r0, rows, stream.cuda_stream)
-            frames.append(b)
-    vworld.check(stream.cuda_stream)
-    torch.cuda.synchronize()
-    vworld.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
-    vworld.set_option(sfrt.SFRT_OPT_VARIANT, 1)
     try:
-        for k, ((p, r, hr, width, height, r0, rows), b) in enumerate(zip(seq, frames)):
-            vworld.set_scene(vs.default_world(p, r, hr), width, height)
-            want = np.full(width * height * 4, 0xA5, dtype=np.uint8)
-            full = vworld.render()
-            want[r0 * width * 4:(r0 + rows) * width * 4] = full[r0 * width * 4:(r0 + rows) * width * 4]
-            assert np.array_equal(b.cpu().numpy().ravel(), want), (k, p, width, height, r0, rows)
-            if k in (0, 11):
-                o = oracle.VoxelOracle(vs.default_world(p, r, hr), width, height, assets[0], assets[1],
-                                       vs.COLORS)
-                assert np.array_equal(full, o.render(host_threads())), k
+        with torch.cuda.stream(stream):
+            for p, r, hr, width, height, r0, rows in seq:
+                vworld.set_scene(vs.default_world(p, r, hr), width, height)
+                b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                vworld.render_band(b[r0].data_ptr(), width * 4, r0, rows, stream.cuda_stream)
+                frames.append(b)
+        vworld.check(stream.cuda_stream)
+        torch.cuda.synchronize()
     finally:
-        vworld.set_option(sfrt.SFRT_OPT_VARIANT, 0)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("variant", [1, 3])
-def test_voxel_kernel_variants_identical(vworld, assets, variant):
-    """SFRT_OPT_VARIANT on the voxel renderer (1: the 2-D-grid kernel; 3: the grid's occupancy
-    bitmask staged in LDS) produces the default kernel's bytes."""
-    import sfrt
-    for case in [(640, 360, (15.5, 1.9, 15.5), 0.0, 0.0), (333, 211, (47.5, 1.5, 60.1), 4.0, -0.3),
-                 (1920, 1080, (30.25, 2.6, 12.75), 2.2, 0.25)]:
-        w, h, p, r, hr = case
-        vworld.set_scene(vs.default_world(p, r, hr), w, h)
-        a = vworld.render()
-        vworld.set_option(sfrt.SFRT_OPT_VARIANT, variant)
-        try:
-            b = vworld.render()
-        finally:
-            vworld.set_option(sfrt.SFRT_OPT_VARIANT, 0)
-        assert np.array_equal(a, b), case
+        vworld.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+    for k, ((p, r, hr, width, height, r0, rows), b) in enumerate(zip(seq, frames)):
+        vworld.set_scene(vs.default_world(p, r, hr), width, height)
+        want = np.full(width * height * 4, 0xA5, dtype=np.uint8)
+        full = vworld.render()
+        want[r0 * width * 4:(r0 + rows) * width * 4] = full[r0 * width * 4:(r0 + rows) * width * 4]
+        assert np.array_equal(b.cpu().numpy().ravel(), want), (k, p, width, height, r0, rows)
+        if k in (0, 11):
+            o = oracle.VoxelOracle(vs.default_world(p, r, hr), width, height, assets[0], assets[1],
+                                   vs.COLORS)
+            assert np.array_equal(full, o.render(host_threads())), k

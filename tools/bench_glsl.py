@@ -25,9 +25,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--variants", default="0", help="SFRT_OPT_VARIANT values to time")
-    ap.add_argument("--orders", default="1",
-                    help="SFRT_OPT_TILE_ORDER values (1 adaptive, 0 row-major; keys get /o0)")
+    ap.add_argument("--orders", default="0",
+                    help="SFRT_OPT_TILE_ORDER values (0 row-major = the default here, 1 adaptive; "
+                         "keys get /ordered)")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -42,14 +42,12 @@ def main():
         u = gs.default_uniforms(width, height, *rot, frames=frames)
         s.set_uniforms(u)
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
-        for var in [int(v) for v in args.variants.split(",")]:
-            for order in [int(v) for v in args.orders.split(",")]:
-                s.set_option(sfrt.SFRT_OPT_VARIANT, var)
-                s.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
-                r = time_one(s, buf, width, height, u, rot, frames, var, args, stream, floor,
-                             threads, oracle)
-                res.update({(k + ("" if order else "/o0")): v for k, v in r.items()})
-        s.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+        for order in [int(v) for v in args.orders.split(",")]:
+            s.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+            r = time_one(s, buf, width, height, u, rot, frames, 0, args, stream, floor,
+                         threads, oracle)
+            res.update({(k + ("/ordered" if order else "")): v for k, v in r.items()})
+        s.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
     print(json.dumps(res, indent=1))
 
 
@@ -80,7 +78,7 @@ def time_one(s, buf, width, height, u, rot, frames, var, args, stream, floor, th
         ent.update({"cpu_Mfrags_per_s": round(width * height / cpu_s / 1e6, 2),
                     "cpu_threads": threads,
                     "bit_identical": bool(np.array_equal(cpu, buf.cpu().numpy().ravel()))})
-    return {f"{width}x{height}@{rot[0]:g},{rot[1]:g}/frames{frames}/v{var}": ent}
+    return {f"{width}x{height}@{rot[0]:g},{rot[1]:g}/frames{frames}": ent}
 
 
 if __name__ == "__main__":

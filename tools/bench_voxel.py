@@ -24,10 +24,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--variants", default="0", help="SFRT_OPT_VARIANT values (keys get /vN)")
-    ap.add_argument("--orders", default="1",
-                    help="comma list of SFRT_OPT_TILE_ORDER values (1 adaptive, 0 row-major; "
-                         "entries get /o0 for row-major)")
+    ap.add_argument("--orders", default="0",
+                    help="comma list of SFRT_OPT_TILE_ORDER values (0 row-major = the default "
+                         "here, 1 adaptive; entries get /ordered)")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -40,12 +39,10 @@ def main():
     frames = [(1920, 1080, ((15.5, 1.9, 15.5), 0.0, 0.0)),
               (3840, 2160, ((15.5, 1.9, 15.5), 0.0, 0.0)),
               (3840, 2160, ((47.5, 1.5, 60.1), 4.0, -0.3))]
-    runs = [(wd, ht, ps, od, vr) for wd, ht, ps in frames
-            for od in [int(x) for x in args.orders.split(",")]
-            for vr in [int(x) for x in args.variants.split(",")]]
-    for width, height, pose, order, var in runs:
+    runs = [(wd, ht, ps, od) for wd, ht, ps in frames
+            for od in [int(x) for x in args.orders.split(",")]]
+    for width, height, pose, order in runs:
         w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
-        w.set_option(sfrt.SFRT_OPT_VARIANT, var)
         scene = vs.default_world(*pose)
         w.set_scene(scene, width, height)
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
@@ -73,8 +70,7 @@ def main():
             ent.update({"cpu_Mrays_per_s": round(width * height / cpu_s / 1e6, 2),
                         "cpu_threads": threads,
                         "bit_identical": bool(np.array_equal(cpu, buf.cpu().numpy().ravel()))})
-        res[f"{width}x{height}@{pose[0]}/{pose[1]},{pose[2]}" + ("" if order else "/o0")
-            + (f"/v{var}" if var else "")] = ent
+        res[f"{width}x{height}@{pose[0]}/{pose[1]},{pose[2]}" + ("/ordered" if order else "")] = ent
     print(json.dumps(res, indent=1))
 
 

@@ -13,7 +13,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
+sys.path.insert(0, HERE)
 
 from pngdecode import load_png_rgba  # noqa: E402
 

@@ -1,5 +1,6 @@
 """Kernel-time ablations in one process (HIP events on one stream), e.g.
     python tools/perf_probe.py            # default variant table
+    SFRT_LIB=path/to/other/libsfrt.so python tools/perf_probe.py   # a build-flag A/B
 Variants isolate the kernel's phases without changing its code:
   march       = scene as given (setup + cull + march + shade)
   nocull      = SFRT_OPT_CULL 0 (every sphere visited)
@@ -42,8 +43,9 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="march,nocull,outside,outside_nc")
-    ap.add_argument("--kvariants", default="0",
-                    help="comma list of SFRT_OPT_VARIANT values, interleaved per round")
+    ap.add_argument("--rays", default="0",
+                    help="comma list of SFRT_OPT_RAYS_PER_LANE values (0 = the kernel table's "
+                         "choice), interleaved per round")
     ap.add_argument("--orders", default="1",
                     help="comma list of SFRT_OPT_TILE_ORDER values (1 adaptive, 0 row-major); "
                          "keys get /o0 for row-major")
@@ -69,16 +71,17 @@ def main():
             allv = (("march", sc, 1), ("nocull", sc, 0), ("outside", outside, 1),
                     ("outside_nc", outside, 0))
             for var, scene, cull in (v for v in allv if v[0] in args.variants.split(",")):
-                for kv in [int(x) for x in args.kvariants.split(",")]:
+                for kv in [int(x) for x in args.rays.split(",")]:
                     for order in [int(x) for x in args.orders.split(",")]:
                         w.set_scene(scene, width, height)
                         w.set_option(sfrt.SFRT_OPT_CULL, cull)
-                        w.set_option(sfrt.SFRT_OPT_VARIANT, kv)
+                        w.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, kv)
                         w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
                         med, best = time_kernel(w, buf, width, height, args.reps, stream)
                         tag = "" if order else "/o0"
-                        out.setdefault(f"{name}/{var}/k{kv}{tag}", []).append(round(med * 1e3, 2))
+                        out.setdefault(f"{name}/{var}/r{kv}{tag}", []).append(round(med * 1e3, 2))
     w.set_option(sfrt.SFRT_OPT_CULL, 1)
+    w.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
     w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
     for k, v in out.items():
         print(f"{k:32s} us(median per round) {v}")

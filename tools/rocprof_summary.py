@@ -26,8 +26,9 @@ import re
 
 
 def pixels_per_thread(kernel_name: str) -> int:
-    """Pixels one work-item writes: R for k_trace_window_r<SLOTS, R>, else 1."""
-    m = re.search(r"k_trace_window_r<\s*\d+\s*,\s*(\d+)", kernel_name)
+    """Pixels one work-item writes: R for k_trace_window_r<R> (round 1: <SLOTS, R, ...>), else 1."""
+    m = re.search(r"k_trace_window_r<\s*(\d+)\s*>", kernel_name) or \
+        re.search(r"k_trace_window_r<\s*\d+\s*,\s*(\d+)", kernel_name)
     return int(m.group(1)) if m else 1
 
 
