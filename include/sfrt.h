@@ -162,6 +162,61 @@ SFRT_API const char* sfrt_error_string(int code);
 SFRT_API int sfrt_version(void);
 
 /* ======================================================================
+ * One frame over several GPUs of this node (BASELINE configs 4-5):
+ * the reference caller is ONE C++ process (Source.cpp:17-28,47-52) that fills
+ * one sf::Image; here it fills it on n GPUs.  The frame is split into
+ * contiguous row bands, rank r = devices[r] renders rows [row0_r, row0_r +
+ * rows_r) with the global row index (so the gathered frame is byte-identical
+ * to a one-GPU render), and the bands travel to devices[0]:
+ *   SFRT_MULTI_RCCL -- RCCL (librccl, loaded at create): one ncclGather for
+ *                      equal bands, grouped ncclSend/ncclRecv otherwise;
+ *   SFRT_MULTI_PEER -- hipMemcpyPeerAsync over xGMI (also serves a device
+ *                      listed twice, which RCCL refuses);
+ *   SFRT_MULTI_AUTO -- RCCL when the devices are distinct, else PEER.
+ * Band transfers run on per-rank copy streams, so frame k's transfer overlaps
+ * frame k+1's render (two band buffers per rank).  The scene setters below
+ * apply to every rank's world; sfrt_multi_world gives a rank's world for
+ * anything else (options).
+ * ====================================================================== */
+typedef struct sfrt_multi sfrt_multi;
+
+#define SFRT_MULTI_AUTO 0
+#define SFRT_MULTI_RCCL 1
+#define SFRT_MULTI_PEER 2
+
+SFRT_API int sfrt_multi_create(const int* hip_devices, int n, int transport, sfrt_multi** out);
+SFRT_API void sfrt_multi_destroy(sfrt_multi* m);
+SFRT_API int sfrt_multi_count(const sfrt_multi* m, int* n, int* transport);
+SFRT_API int sfrt_multi_world(sfrt_multi* m, int rank, sfrt_world** out);
+SFRT_API int sfrt_multi_set_size(sfrt_multi* m, int width, int height);
+SFRT_API int sfrt_multi_set_camera(sfrt_multi* m, const sfrt_camera* cam);
+SFRT_API int sfrt_multi_load_texture(sfrt_multi* m, int slot, const uint8_t* rgba, int tex_w, int tex_h);
+SFRT_API int sfrt_multi_set_spheres(sfrt_multi* m, const sfrt_sphere* spheres, int count);
+SFRT_API int sfrt_multi_add_sphere(sfrt_multi* m, float x, float y, float z, float radius);
+SFRT_API int sfrt_multi_update_spheres(sfrt_multi* m);
+SFRT_API int sfrt_multi_set_sphere_textures(sfrt_multi* m, const int32_t* slots, int count);
+SFRT_API int sfrt_multi_set_option(sfrt_multi* m, int option, int value);
+/* Band heights: rows[r] for rank r (rank 0 first, sum = height at render time);
+ * rows == NULL restores the default equal split (sfrt_multi_bands, factor 1). */
+SFRT_API int sfrt_multi_set_bands(sfrt_multi* m, const int* rows, int n);
+/* The partition helper (stateless, no device): row0/rows of n ranks for a frame
+ * of `height` rows where rank 0 -- whose band never crosses a link -- gets about
+ * `root_factor` times the rows of every other rank (their bands equal and
+ * multiples of the 8-row tile); root_factor 1 = equal split
+ * [r*H/n, (r+1)*H/n). */
+SFRT_API int sfrt_multi_bands(int height, int n, float root_factor, int* row0, int* rows);
+/* Render the whole width x height frame into `dev_frame` (device memory on
+ * devices[0], pitch exactly width*4), asynchronously: every rank starts after
+ * the work already queued on `hip_stream` (a stream of devices[0]; NULL = null
+ * stream), and the frame is complete when `hip_stream` reaches the point after
+ * this call.  sfrt_multi_check synchronises and reads every rank's status. */
+SFRT_API int sfrt_multi_render(sfrt_multi* m, void* dev_frame, int64_t pitch_bytes, void* hip_stream);
+SFRT_API int sfrt_multi_check(sfrt_multi* m);
+/* UpdateImage(v, 0, 1, 0, 1) on n GPUs: the whole frame into the caller's host
+ * RGBA8 buffer (width*height*4 bytes, pitch 4*width).  Synchronous. */
+SFRT_API int sfrt_multi_update_image(sfrt_multi* m, uint8_t* pixels);
+
+/* ======================================================================
  * Voxel World frame fill: drop-in for
  *   void World::UpdateImage(sf::Image* v, short ystart, short yadd,
  *                           short xstart, short xadd)

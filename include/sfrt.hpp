@@ -5,6 +5,8 @@
 // mutates and whose frame fill reads it (paths under /root/reference/Raytracing/):
 //   sfrt::SphereWorld  <- class SphereWorld (SphereWorld.h:40-78): width,
 //                         height, cam, AddSphere, UpdateSpheres, UpdateImage
+//   sfrt::MultiSphereWorld <- the same SphereWorld, its frame filled by several
+//                         GPUs of the node (row bands gathered on the first one)
 //   sfrt::VoxelWorld   <- class World (World.h:58-97): width, height, cam,
 //                         shadowDistance, viewDistance, UpdateImage
 //   sfrt::Shader       <- sf::Shader running rayShader.frag: setUniform by name,
@@ -176,6 +178,77 @@ class SphereWorld {
     push_camera();
   }
   sfrt_world* w_ = nullptr;
+};
+
+// ---------------------------------------------------------------------------
+// MultiSphereWorld: SphereWorld's state and frame fill over the GPUs `devices`
+// (sfrt_multi_*: row bands with global row indices, gathered on devices[0] by
+// RCCL or peer copies).  UpdateImage fills the whole frame, as the reference's
+// eight RenderThreads together do once per full cycle (Source.cpp:17-28).
+class MultiSphereWorld {
+ public:
+  int width = 320;
+  int height = 180;
+  Camera cam;
+
+  explicit MultiSphereWorld(const std::vector<int>& devices, int transport = SFRT_MULTI_AUTO) {
+    check(sfrt_multi_create(devices.data(), (int)devices.size(), transport, &m_),
+          "sfrt_multi_create");
+    sfrt_world* w0 = nullptr;
+    sfrt_multi_world(m_, 0, &w0);
+    sfrt_camera c;
+    sfrt_world_get_camera(w0, &c);
+    cam.fovH = c.fov_h;
+    cam.fovV = c.fov_v;
+  }
+  ~MultiSphereWorld() { sfrt_multi_destroy(m_); }
+  MultiSphereWorld(const MultiSphereWorld&) = delete;
+  MultiSphereWorld& operator=(const MultiSphereWorld&) = delete;
+
+  void LoadTexture(const Image& img) {
+    check(sfrt_multi_load_texture(m_, 0, img.pixels.data(), img.width, img.height),
+          "multi_load_texture");
+  }
+  void AddSphere(Vector3f pos, float radius) {
+    push_camera();
+    check(sfrt_multi_add_sphere(m_, pos.x, pos.y, pos.z, radius), "AddSphere");
+  }
+  void UpdateSpheres() {
+    push_camera();
+    check(sfrt_multi_update_spheres(m_), "UpdateSpheres");
+  }
+  void SetSpheres(const std::vector<sfrt_sphere>& s) {
+    check(sfrt_multi_set_spheres(m_, s.data(), (int)s.size()), "set_spheres");
+  }
+  // Rows per GPU (rank 0 first; empty = equal bands).
+  void SetBands(const std::vector<int>& rows) {
+    check(sfrt_multi_set_bands(m_, rows.empty() ? nullptr : rows.data(), (int)rows.size()),
+          "set_bands");
+  }
+  // The whole frame into a caller-owned sf::Uint8* RGBA8 buffer (width*height*4).
+  void UpdateImage(uint8_t* pixels) {
+    push_state();
+    check(sfrt_multi_update_image(m_, pixels), "UpdateImage");
+  }
+  // The whole frame into device memory on devices[0] (pitch width*4), queued after
+  // hip_stream's work; complete when hip_stream passes this point.
+  void Render(void* dev_frame, void* hip_stream) {
+    push_state();
+    check(sfrt_multi_render(m_, dev_frame, (int64_t)width * 4, hip_stream), "render");
+  }
+  void Check() { check(sfrt_multi_check(m_), "check"); }
+  sfrt_multi* handle() { return m_; }
+
+ private:
+  void push_camera() {
+    const sfrt_camera c = to_c(cam);
+    check(sfrt_multi_set_camera(m_, &c), "set_camera");
+  }
+  void push_state() {
+    check(sfrt_multi_set_size(m_, width, height), "set_size");
+    push_camera();
+  }
+  sfrt_multi* m_ = nullptr;
 };
 
 // ---------------------------------------------------------------------------

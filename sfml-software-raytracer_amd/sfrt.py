@@ -47,7 +47,14 @@ ABI_SYMBOLS = (
     "sfrt_glsl_get_uniforms", "sfrt_glsl_set_uniform", "sfrt_glsl_set_uniform_int",
     "sfrt_glsl_draw", "sfrt_glsl_draw_image", "sfrt_glsl_check", "sfrt_glsl_set_option",
     "sfrt_png_info", "sfrt_png_decode",
+    "sfrt_multi_create", "sfrt_multi_destroy", "sfrt_multi_count", "sfrt_multi_world",
+    "sfrt_multi_set_size", "sfrt_multi_set_camera", "sfrt_multi_load_texture",
+    "sfrt_multi_set_spheres", "sfrt_multi_add_sphere", "sfrt_multi_update_spheres",
+    "sfrt_multi_set_sphere_textures", "sfrt_multi_set_option", "sfrt_multi_set_bands",
+    "sfrt_multi_bands", "sfrt_multi_render", "sfrt_multi_check", "sfrt_multi_update_image",
 )
+
+SFRT_MULTI_AUTO, SFRT_MULTI_RCCL, SFRT_MULTI_PEER = 0, 1, 2
 
 
 class SfrtError(RuntimeError):
@@ -151,6 +158,23 @@ def lib() -> ctypes.CDLL:
         "sfrt_glsl_set_option": ([vp, c_int, c_int], c_int),
         "sfrt_png_info": ([vp, ctypes.c_int64, P(c_int), P(c_int)], c_int),
         "sfrt_png_decode": ([vp, ctypes.c_int64, vp, ctypes.c_int64, P(c_int), P(c_int)], c_int),
+        "sfrt_multi_create": ([vp, c_int, c_int, P(vp)], c_int),
+        "sfrt_multi_destroy": ([vp], None),
+        "sfrt_multi_count": ([vp, P(c_int), P(c_int)], c_int),
+        "sfrt_multi_world": ([vp, c_int, P(vp)], c_int),
+        "sfrt_multi_set_size": ([vp, c_int, c_int], c_int),
+        "sfrt_multi_set_camera": ([vp, P(Camera)], c_int),
+        "sfrt_multi_load_texture": ([vp, c_int, vp, c_int, c_int], c_int),
+        "sfrt_multi_set_spheres": ([vp, vp, c_int], c_int),
+        "sfrt_multi_add_sphere": ([vp, c_float, c_float, c_float, c_float], c_int),
+        "sfrt_multi_update_spheres": ([vp], c_int),
+        "sfrt_multi_set_sphere_textures": ([vp, vp, c_int], c_int),
+        "sfrt_multi_set_option": ([vp, c_int, c_int], c_int),
+        "sfrt_multi_set_bands": ([vp, vp, c_int], c_int),
+        "sfrt_multi_bands": ([c_int, c_int, c_float, vp, vp], c_int),
+        "sfrt_multi_render": ([vp, vp, ctypes.c_int64, vp], c_int),
+        "sfrt_multi_check": ([vp], c_int),
+        "sfrt_multi_update_image": ([vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -442,6 +466,99 @@ class VoxelWorld:
 
     def set_option(self, option: int, value: int) -> None:
         _check(lib().sfrt_voxel_set_option(self._h, option, value), "voxel_set_option")
+
+
+def multi_bands(height: int, n: int, root_factor: float = 1.0) -> list[tuple[int, int]]:
+    """sfrt_multi_bands: (row0, rows) per rank, rank 0 ~root_factor x the others' rows."""
+    row0 = np.zeros(n, dtype=np.int32)
+    rows = np.zeros(n, dtype=np.int32)
+    _check(lib().sfrt_multi_bands(int(height), int(n), float(root_factor), row0.ctypes.data,
+                                  rows.ctypes.data), "sfrt_multi_bands")
+    return [(int(a), int(b)) for a, b in zip(row0, rows)]
+
+
+class Multi:
+    """One frame over several GPUs of this node through the C ABI (sfrt_multi_*): the scene
+    setters of ``World`` broadcast to one world per device, the frame is rendered in row
+    bands and gathered on devices[0] (RCCL or peer copies)."""
+
+    def __init__(self, devices, transport: int = SFRT_MULTI_AUTO):
+        devs = np.ascontiguousarray(np.asarray(devices, dtype=np.int32))
+        h = ctypes.c_void_p()
+        _check(lib().sfrt_multi_create(devs.ctypes.data, devs.size, int(transport),
+                                       ctypes.byref(h)), "sfrt_multi_create")
+        self._h = h
+        self.devices = [int(d) for d in devs]
+        self.width = self.height = 0
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().sfrt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def transport(self) -> int:
+        n, t = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sfrt_multi_count(self._h, ctypes.byref(n), ctypes.byref(t)), "multi_count")
+        return t.value
+
+    def load_texture(self, rgba, tex_w: int, tex_h: int, slot: int = 0) -> None:
+        buf = np.ascontiguousarray(np.asarray(rgba, dtype=np.uint8).ravel())
+        _check(lib().sfrt_multi_load_texture(self._h, slot, buf.ctypes.data, tex_w, tex_h),
+               "multi_load_texture")
+
+    def set_camera(self, pos, rotation=0.0, hrotation=0.0, fov_h=None, fov_v=None) -> None:
+        cam = Camera()
+        for k in range(3):
+            cam.pos[k] = float(pos[k])
+        cam.rotation, cam.hrotation = float(rotation), float(hrotation)
+        cam.fov_h = float(fov_h) if fov_h is not None else float(deg_to_rad(75.0))
+        cam.fov_v = float(fov_v) if fov_v is not None else float(deg_to_rad(47.0))
+        _check(lib().sfrt_multi_set_camera(self._h, ctypes.byref(cam)), "multi_set_camera")
+
+    def set_scene(self, scene, width: int, height: int) -> None:
+        self.width, self.height = int(width), int(height)
+        _check(lib().sfrt_multi_set_size(self._h, self.width, self.height), "multi_set_size")
+        self.set_camera(scene.cam_pos, scene.rotation, scene.hrotation, scene.fov_h, scene.fov_v)
+        s = _f32_rows(scene.spheres)
+        _check(lib().sfrt_multi_set_spheres(self._h, s.ctypes.data, s.shape[0]), "multi_set_spheres")
+
+    def set_option(self, option: int, value: int) -> None:
+        _check(lib().sfrt_multi_set_option(self._h, option, value), "multi_set_option")
+
+    def set_bands(self, rows=None) -> None:
+        if rows is None:
+            _check(lib().sfrt_multi_set_bands(self._h, None, 0), "multi_set_bands")
+            return
+        r = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
+        _check(lib().sfrt_multi_set_bands(self._h, r.ctypes.data, r.size), "multi_set_bands")
+
+    def render(self, dev_ptr: int, pitch_bytes: int, stream: int = 0) -> None:
+        _check(lib().sfrt_multi_render(self._h, ctypes.c_void_p(dev_ptr), int(pitch_bytes),
+                                       ctypes.c_void_p(stream or None)), "multi_render")
+
+    def check(self) -> None:
+        _check(lib().sfrt_multi_check(self._h), "multi_check")
+
+    def update_image(self, pixels=None) -> np.ndarray:
+        if pixels is None:
+            pixels = np.zeros(self.width * self.height * 4, dtype=np.uint8)
+        if pixels.dtype != np.uint8 or pixels.size != self.width * self.height * 4:
+            raise ValueError("pixels must be uint8 width*height*4")
+        _check(lib().sfrt_multi_update_image(self._h, pixels.ctypes.data), "multi_update_image")
+        return pixels
 
 
 def decode_png(data: bytes) -> tuple[np.ndarray, int, int]:

@@ -124,3 +124,34 @@ def test_cpp_header_builds(built, tmp_path):
                     "-lsfrt", f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath-link,/opt/rocm/lib",
                     "-lpthread", "-o", str(exe)], check=True)
     assert exe.exists()
+
+
+def test_multi_bands_match_band_tuner(lib):
+    """sfrt_multi_bands (the C-ABI partition of sfrt_multi) equals bands.root_weighted_spans
+    (the partition the torch.distributed path tunes), row for row, and tiles the frame."""
+    import bands
+    import sfrt
+    for world_size in (1, 2, 3, 4, 8):
+        for height in (0, 1, 7, 90, 1080, 2160, 4320, 16384, 17280):
+            for factor in (1.0,) + bands.DEFAULT_FACTORS + (0.5, 10.0):
+                got = sfrt.multi_bands(height, world_size, factor)
+                assert got == bands.root_weighted_spans(height, world_size, factor), \
+                    (height, world_size, factor)
+                bands.check_spans(got, height)
+    assert sfrt.multi_bands(4320, 2) == [(0, 2160), (2160, 2160)]
+    assert sfrt.multi_bands(16384, 8) == [(r * 2048, 2048) for r in range(8)]
+    with pytest.raises(sfrt.SfrtError):
+        sfrt.multi_bands(100, 0)
+    with pytest.raises(sfrt.SfrtError):
+        sfrt.multi_bands(100, 2, float("nan"))
+
+
+def test_multi_create_without_gpu_fails_loudly(lib):
+    import sfrt
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    devs = (ctypes.c_int * 2)(0, 1)
+    h = ctypes.c_void_p()
+    assert lib.sfrt_multi_create(devs, 2, sfrt.SFRT_MULTI_AUTO, ctypes.byref(h)) == -5
+    assert lib.sfrt_multi_create(devs, 0, sfrt.SFRT_MULTI_AUTO, ctypes.byref(h)) == -1

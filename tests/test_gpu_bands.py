@@ -1,0 +1,174 @@
+"""BASELINE configs 4 and 5 in their row-banded, gathered form, on the GPU.
+
+Config 4 is "7680x4320 row-tiled across 2 and 4 GPUs", config 5 "16384x16384, 8x
+MI355X".  A one-GPU box cannot give each rank its own device, so the ranks here
+share cuda:0 -- the band math, global row indices, offsets and the exchange are
+the same code a node runs:
+
+* torch.distributed (bench.py's N > 1 path): world_size 2 / 4 / 8 processes, each
+  rendering its band through libsfrt.so's sfrt_world_render_band, assembled on
+  rank 0 by bands.BandPipeline (gloo on host copies of the bands: RCCL refuses
+  two ranks on one device);
+* the C ABI (sfrt_multi_*, the single-process caller of Source.cpp:17-28):
+  devices [0] * n with peer copies, and [0] with RCCL.
+
+Every gathered frame's FNV-1a-64 must equal the oracle's golden hash of the
+whole frame (tests/golden/golden.json, c4_* and c5_*), for equal bands and for
+root-weighted bands (rank 0 renders more rows; point-to-point transfers).
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import scenes
+from conftest import ROOT, host_threads
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _band_worker(rank, world_size, port, key, factor, frames, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), os.path.join(ROOT, "oracle"), ROOT):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import bands
+    import oracle
+    import scenes as sc
+    import sfrt
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world_size)
+    g = GOLDEN["frames"][key]
+    width, height = g["width"], g["height"]
+    pitch = width * 4
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    w = sfrt.World(0)
+    w.load_texture(*sc.load_floor())
+    w.set_scene(sc.SCENES[g["scene"]]().posed(*g["pose"]), width, height)
+    spans = bands.root_weighted_spans(height, world_size, factor)
+    pipe = bands.BandPipeline(rank, world_size, height, pitch, "cpu", spans=spans)
+    dev = torch.empty(max(pipe.rows, 1), pitch, dtype=torch.uint8, device="cuda:0")
+    for k in range(frames):
+        band = pipe.acquire(k)
+        if pipe.rows:
+            w.render_band(dev.data_ptr(), pitch, pipe.row0, pipe.rows, stream.cuda_stream)
+            w.check(stream.cuda_stream)
+            band.copy_(dev[:pipe.rows].cpu())
+        pipe.submit(k)
+    pipe.drain()
+    w.close()
+    if rank == 0:
+        got = [oracle.fnv1a64(pipe.frame(k).numpy()) for k in range(frames)]
+        np.save(out_path, np.array([h == g["fnv1a64"] for h in got] + [len(got) == frames]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("key,world_size,factor", [
+    ("c4_7680x4320_lcg64@0,0", 2, 1.0), ("c4_7680x4320_lcg64@0,0", 4, 1.0),
+    ("c4_7680x4320_default10@0,0", 2, 1.0), ("c4_7680x4320_default10@0,0", 4, 1.0),
+    ("c4_7680x4320_lcg64@0,0", 2, 2.5), ("c4_7680x4320_default10@0,0", 4, 2.0),
+    ("c5_16384x16384_default10@0,0", 8, 1.0)])
+def test_distributed_bands_match_golden(tmp_path, key, world_size, factor):
+    """world_size ranks on cuda:0, HIP-rendered bands, gathered to rank 0 by BandPipeline
+    (two frames in flight for config 4): the frames hash to the single-frame golden value."""
+    out = str(tmp_path / "ok.npy")
+    frames = 1 if key.startswith("c5") else 2
+    mp.start_processes(_band_worker, args=(world_size, _free_port(), key, factor, frames, out),
+                       nprocs=world_size, start_method="spawn", join=True)
+    assert np.load(out).all()
+
+
+@pytest.fixture(scope="module")
+def floor_tex(built):
+    return scenes.load_floor()
+
+
+def _multi(devices, transport, floor_tex):
+    import sfrt
+    m = sfrt.Multi(devices, transport)
+    m.load_texture(*floor_tex)
+    return m
+
+
+@pytest.mark.parametrize("key,n,factor", [
+    ("c4_7680x4320_lcg64@0,0", 2, 1.0), ("c4_7680x4320_lcg64@0,0", 4, 1.0),
+    ("c4_7680x4320_default10@0,0", 2, 2.5), ("c4_7680x4320_default10@0,0", 4, 2.0),
+    ("c5_16384x16384_default10@0,0", 8, 1.0)])
+def test_multi_peer_matches_golden(floor_tex, key, n, factor):
+    """sfrt_multi over devices [0] * n (peer copies into devices[0]'s frame): the host frame
+    of sfrt_multi_update_image hashes to the golden value, equal and root-weighted bands."""
+    import oracle
+    import sfrt
+    g = GOLDEN["frames"][key]
+    with _multi([0] * n, sfrt.SFRT_MULTI_PEER, floor_tex) as m:
+        assert m.transport == sfrt.SFRT_MULTI_PEER
+        m.set_scene(scenes.SCENES[g["scene"]]().posed(*g["pose"]), g["width"], g["height"])
+        if factor != 1.0:
+            m.set_bands([r for _, r in sfrt.multi_bands(g["height"], n, factor)])
+        assert oracle.fnv1a64(m.update_image()) == g["fnv1a64"]
+
+
+def test_multi_rccl_one_gpu_matches_oracle(floor_tex):
+    """sfrt_multi with RCCL (ncclCommInitAll over [0], one in-place ncclGather): frames equal
+    the oracle's; the AUTO transport picks RCCL for distinct devices and peer copies for a
+    device listed twice; RCCL over a repeated device is refused."""
+    import oracle
+    import sfrt
+    width, height = 640, 360
+    with _multi([0], sfrt.SFRT_MULTI_AUTO, floor_tex) as m:
+        assert m.transport == sfrt.SFRT_MULTI_RCCL
+        for pose in [(0.0, 0.0), (1.1, -0.2)]:
+            sc = scenes.lcg64().posed(*pose)
+            m.set_scene(sc, width, height)
+            want = oracle.Oracle.from_scene(sc, width, height, *floor_tex).render(host_threads())
+            assert np.array_equal(m.update_image(), want), pose
+    with _multi([0, 0], sfrt.SFRT_MULTI_AUTO, floor_tex) as m:
+        assert m.transport == sfrt.SFRT_MULTI_PEER
+    with pytest.raises(sfrt.SfrtError):
+        sfrt.Multi([0, 0], sfrt.SFRT_MULTI_RCCL)
+
+
+@pytest.mark.parametrize("n,transport", [(1, 1), (3, 2)])
+def test_multi_render_pipelined_frames(floor_tex, n, transport):
+    """sfrt_multi_render into device frames on a caller's stream, six frames queued back to
+    back (two band buffers per rank, transfers overlapping the next render), the camera
+    turning every frame, 1000 x 563 (ragged bands): each frame equals a one-GPU World frame."""
+    import sfrt
+    import torch
+    width, height = 1000, 563
+    sc = scenes.lcg64()
+    poses = [(0.3 * k, 0.05 * k - 0.1) for k in range(6)]
+    ref = sfrt.World(0)
+    ref.load_texture(*floor_tex)
+    want = []
+    for p in poses:
+        ref.set_scene(sc.posed(*p), width, height)
+        want.append(ref.render())
+    ref.close()
+    stream = torch.cuda.Stream()
+    with _multi([0] * n, transport, floor_tex) as m:
+        m.set_scene(sc, width, height)
+        frames = []
+        with torch.cuda.stream(stream):
+            for p in poses:
+                m.set_camera(sc.cam_pos, *p)
+                f = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                m.render(f.data_ptr(), width * 4, stream.cuda_stream)
+                frames.append(f)
+        m.check()
+        torch.cuda.synchronize()
+        for k, f in enumerate(frames):
+            assert np.array_equal(f.cpu().numpy().ravel(), want[k]), k
