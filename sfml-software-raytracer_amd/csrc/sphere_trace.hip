@@ -25,6 +25,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef SFRT_EXP
+#define SFRT_EXP 0  // build-flag A/B knobs (tools/ab_libs.py); 0 = the shipped kernel
+#endif
+
 namespace sfrt {
 namespace {
 
@@ -174,7 +178,16 @@ __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereR
           const float sb = perp * c.cos_t + t * c.sin_t;  // |w| sin(alpha + theta)
           const float up = sa >= 0.0f ? t * c.cos_t + perp * c.sin_t : wl;
           const float dn = sb >= 0.0f ? t * c.cos_t - perp * c.sin_t : -wl;
-          const float ext = rr + f.cull_margin;
+          // Half-width: a ray whose line passes the centre at distance d has |q - c|^2 =
+          // (tau - dot(w, u))^2 + d^2 at its exact point q(tau), so a pass (|q - c| < rr)
+          // needs |tau - dot(w, u)| < sqrt(rr^2 - d^2).  Over the cone d >= |w| *
+          // min(sin(alpha - theta), sin(alpha + theta)) = min(sa, sb) when both are >= 0
+          // (else the cone's angles reach 0 or pi and d can be 0), taken 4e-6 |w| lower
+          // for the binary32 error of sa and sb; the product form keeps the root's
+          // relative error at a few ulps, and the 1e-5 relative slack covers it.
+          const float dmin = fmaxf(0.0f, fminf(sa, sb) - 4e-6f * wl);
+          const float h = __builtin_sqrtf((rr - dmin) * (rr + dmin)) * 1.00001f;
+          const float ext = h + f.cull_margin;
           lo = dn - ext;
           hi = up + ext;
         }
@@ -458,10 +471,23 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       int dnew[R];
 #pragma unroll
       for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
-      for (uint64_t mm = win; mm; mm &= mm - 1) {
-        const int k = __builtin_ctzll(mm);
-        const SphereRec& s = sph[k];
-        visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      // The visits, in index order, each issuing the next record's scalar loads before
+      // its own arithmetic (the loads' latency hides under the R rays' distance tests;
+      // kn = k for the last visit reloads a record already in the scalar cache).
+      if (win) {
+        uint64_t mm = win;
+        int k = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
+        for (;;) {
+          const int kn = mm ? __builtin_ctzll(mm) : k;
+          const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
+                      nsp = sph[kn].s_pass;
+          visit(cx, cy, cz, rad, sp, k, L, dnew);
+          if (!mm) break;
+          mm &= mm - 1;
+          k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
+        }
       }
       advance(L, dnew);
     }

@@ -1,0 +1,113 @@
+"""Build-flag A/B of libsfrt.so builds, interleaved across processes, bytes checked.
+
+    python tools/ab_libs.py --libs a.so,b.so [--rounds 3] [--reps 40] [--cases 4k,4k_rot,...]
+
+Each round starts one process per library (SFRT_LIB=<lib>, the same sfrt.py), which
+times every case with HIP events (median kernel time, event-pair overhead subtracted;
+adaptive tile order, frames back to back on one stream, camera turning in the *_turn
+cases) and hashes one frame per case.  The parent prints per-case medians over rounds
+and fails if any library's frame hash differs from the first library's.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = {
+    "4k": (3840, 2160, "lcg64", (0.0, 0.0), False),
+    "4k_rot": (3840, 2160, "lcg64", (1.1, -0.2), False),
+    "4k_turn": (3840, 2160, "lcg64", (0.0, 0.0), True),
+    "8k": (7680, 4320, "lcg64", (0.0, 0.0), False),
+    "1080": (1920, 1080, "default10", (0.0, 0.0), False),
+    "4k_256": (3840, 2160, "lcg256", (0.0, 0.0), False),
+}
+
+
+def child(cases, reps):
+    sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import torch
+    import oracle
+    import scenes
+    import sfrt
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    w = sfrt.World(0)
+    w.load_texture(*scenes.load_floor())
+    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+             for _ in range(64)]
+    for a, b in pairs:
+        a.record(stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    gap = float(np.median([a.elapsed_time(b) for a, b in pairs]))
+    out = {}
+    for name in cases:
+        width, height, sname, pose, turn = CASES[name]
+        sc = scenes.SCENES[sname]().posed(*pose)
+        w.set_scene(sc, width, height)
+        buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
+        for k in range(20):  # warm-up (clock ramp, tile-order chain)
+            if turn:
+                w.set_camera(sc.cam_pos, 0.004 * k, 0.0)
+            w.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(reps)]
+        for k, (a, b) in enumerate(ev):
+            if turn:
+                w.set_camera(sc.cam_pos, 0.004 * (20 + k), 0.0)
+            a.record(stream)
+            w.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+            b.record(stream)
+        torch.cuda.synchronize()
+        w.check(stream.cuda_stream)
+        t = sorted(a.elapsed_time(b) for a, b in ev)
+        out[name] = {"us": round((t[len(t) // 2] - gap) * 1e3, 2),
+                     "fnv": oracle.fnv1a64(buf.cpu().numpy())}
+    print("RESULT " + json.dumps(out), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=40)
+    ap.add_argument("--cases", default="4k,4k_rot,4k_turn,8k,1080")
+    ap.add_argument("--child", action="store_true")
+    a = ap.parse_args()
+    cases = a.cases.split(",")
+    if a.child:
+        child(cases, a.reps)
+        return
+    libs = a.libs.split(",")
+    res = {lib: {c: [] for c in cases} for lib in libs}
+    hashes = {}
+    for rnd in range(a.rounds):
+        for lib in libs:
+            env = dict(os.environ, SFRT_LIB=os.path.abspath(lib))
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
+                                "--cases", a.cases, "--reps", str(a.reps)],
+                               capture_output=True, text=True, env=env, timeout=600)
+            line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
+            if r.returncode != 0 or not line:
+                print(r.stdout[-2000:], r.stderr[-2000:])
+                raise SystemExit(f"{lib}: child failed")
+            d = json.loads(line[0][7:])
+            for c in cases:
+                res[lib][c].append(d[c]["us"])
+                hashes.setdefault(c, d[c]["fnv"])
+                if d[c]["fnv"] != hashes[c]:
+                    raise SystemExit(f"{lib}: {c} bytes differ ({d[c]['fnv']} vs {hashes[c]})")
+    summary = {}
+    for lib in libs:
+        summary[lib] = {c: sorted(v)[len(v) // 2] for c, v in res[lib].items()}
+        print(f"{lib:40s} " + "  ".join(f"{c} {summary[lib][c]:8.2f}" for c in cases))
+    print(json.dumps({"median_us": summary, "rounds": res, "bytes_identical": True}))
+
+
+if __name__ == "__main__":
+    main()
