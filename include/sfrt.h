@@ -137,10 +137,10 @@ SFRT_API int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count
 
 /* Options: SFRT_OPT_CULL (1 = per-wave sphere culling, default; 0 = visit
  * every sphere -- same bytes, slower; used by A/B parity tests).
- * SFRT_OPT_RAYS_PER_LANE (0 = default): pixels per lane of the <= 64-sphere
- * kernel, i.e. its (8R)x8 tile width; 1-4 force that kernel (parity tests run
- * every shipped tile shape through it; same bytes), 0 lets the kernel table
- * choose (sphere_trace.hip trace_rays).  Ignored above 64 spheres.
+ * SFRT_OPT_RAYS_PER_LANE (0 = default): pixels per lane R of the frame-fill
+ * kernel, i.e. its (8R)x8 tile width; 1-4 force that shape (parity tests run
+ * every shipped tile shape; same bytes), 0 lets the kernel table choose
+ * (sphere_trace.hip trace_rays).
  * SFRT_OPT_TILE_ORDER (1 = default): sfrt_world_render_band dispatches the tiles
  * of a frame longest-first by the march steps an earlier render_band of the same
  * geometry recorded (two frames back; the sort runs inside the next launch);

@@ -13,10 +13,8 @@
 namespace sfrt {
 
 constexpr int kInlineSpheres = 64;    // spheres carried in the kernel-argument segment
-constexpr int kMaxSpheres = 1024;     // 16 culling words of 64 spheres per wave
-constexpr int kMaskWords = kMaxSpheres / 64;
-constexpr int kTile = 8;              // one wave64 = one 8x8 pixel tile
-constexpr int kWavesPerBlock = 4;     // 256-thread workgroups
+constexpr int kMaxSpheres = 1024;     // 16 culling words of 64 spheres, compacted per wave
+constexpr int kTile = 8;              // tile rows; a wave's tile is (8R) x 8 pixels
 constexpr int kMaxIterations = 1 << 20;  // march guard; the reference has none
 // Per-wave culling is proven safe while every lane of the wave has made at
 // most this many march steps (the accumulated binary32 error of the march
@@ -24,7 +22,7 @@ constexpr int kMaxIterations = 1 << 20;  // march guard; the reference has none
 // goes further switches to the full sphere list for the rest of its march.
 constexpr int kCullSafeIterations = 1024;
 constexpr int kPairMinSpheres = 16;  // above this, n <= 64 frames use 16x8 tiles (2 px per lane)
-constexpr int kSlots = 4;             // culled spheres held in SGPRs per wave (measured best of 0,4,6,8)
+constexpr int kSlots = 2;  // culled spheres held in SGPRs per wave (measured best of 0-4, 6; tools/ab_libs.py)
 
 // One sphere as the kernel reads it: 32 B, one s_load_dwordx8.
 struct SphereRec {

@@ -104,30 +104,6 @@ struct Cone {
   bool wide;
 };
 
-__device__ __forceinline__ Cone tile_cone(const FrameRec& f, int tile_x, int tile_y, float dx,
-                                          float dy, float dz) {
-  const float ic = (float)f.xstart + ((float)(tile_x * kTile) + 3.5f) * (float)f.xadd;
-  const float jc = (float)f.ystart +
-                   ((float)(f.sub_row0 + tile_y * kTile) + 3.5f) * (float)f.yadd;
-  const float h = f.h_start + f.h_inc * ic;
-  const float v = f.v_start + jc * f.v_inc;
-  float ax = (f.fwd[0] + f.right[0] * h) + f.up[0] * v;
-  float ay = (f.fwd[1] + f.right[1] * h) + f.up[1] * v;
-  float az = (f.fwd[2] + f.right[2] * h) + f.up[2] * v;
-  const float inv = __builtin_amdgcn_rsqf((ax * ax + ay * ay) + az * az);
-  ax *= inv; ay *= inv; az *= inv;
-  const float cx = dy * az - dz * ay, cy = dz * ax - dx * az, cz = dx * ay - dy * ax;
-  const float sin_l = __builtin_sqrtf((cx * cx + cy * cy) + cz * cz);
-  const float cos_l = (dx * ax + dy * ay) + dz * az;
-  Cone c;
-  c.ax = ax; c.ay = ay; c.az = az;
-  // sin_l >= +0 (inputs finite, sfrt_world.cpp): max over the bit patterns
-  c.sin_t = fminf(1.0f, __uint_as_float(wave_max_u32(__float_as_uint(sin_l))) + 1e-5f);
-  c.cos_t = __builtin_sqrtf(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
-  c.wide = __builtin_amdgcn_ballot_w64(cos_l < 0.5f) != 0;  // min over lanes < 0.5
-  return c;
-}
-
 // Wave-level cull ("wavefront ballot") plus march window.  Lane l tests sphere
 // base + l against the cone; bit l of the result is set when the sphere may
 // pass the march test for some ray of the wave's tile.  A sphere is dropped
@@ -143,15 +119,16 @@ __device__ __forceinline__ Cone tile_cone(const FrameRec& f, int tile_x, int til
 // sphere base + l, an interval (lo, hi) of along-ray distance outside which
 // the sphere cannot pass for any ray of the cone.  A ray's march position p
 // at along-ray distance tau lies within the drift bound of the ray's point
-// cam + u*tau (cull_margin), and |cam + u*tau - c| >= |tau - dot(c - cam, u)|,
-// so a pass needs |tau - dot(w, u)| < r + drift.  Over the cone's rays
-// dot(w, u) = |w| cos(angle(w, u)) with the angle in
+// cam + u*tau (cull_margin), so a pass needs |cam + u*tau - c| < rr, i.e.
+// |tau - dot(w, u)| < sqrt(rr^2 - d^2) with d the distance of the centre from
+// the ray's line (the half-width h below bounds it over the cone).  Over the
+// cone's rays dot(w, u) = |w| cos(angle(w, u)) with the angle in
 // [max(0, alpha - theta), min(pi, alpha + theta)] (alpha = angle(w, axis),
 // theta = half-angle): |w| cos(alpha -+ theta) = t cos_t +- perp sin_t,
 // clamped to +-|w| where alpha - theta < 0 or alpha + theta > pi.  The
-// interval is widened by r + 2 * cull_margin: the drift, the binary32 error
-// of the lanes' accumulated distance (<= 1.3e-4 R over kCullSafeIterations
-// steps) and of these expressions all fit in the second margin.
+// interval is widened by h + cull_margin: the binary32 error of the lanes'
+// accumulated distance (<= 1.3e-4 R over kCullSafeIterations steps) and of
+// these expressions fit in the second margin.
 __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereRec* __restrict__ sph,
                                                 int base, const Cone& c, float& lo, float& hi) {
   const int k = base + (int)(threadIdx.x & 63);
@@ -205,24 +182,6 @@ __device__ __forceinline__ float max_nonneg(float L, float t) {
   return __uint_as_float(__builtin_elementwise_max(__float_as_uint(L), __float_as_uint(t)));
 }
 
-// Pass body of a sphere test (SphereWorld.cpp:366-368) for the lanes in
-// `pass`: t = r - sqrtf(ss) exactly; largestDist = max; drawSphere = k.
-__device__ __forceinline__ void pass_body(bool pass, float ss, float r, int k, float& L,
-                                          int& dnew) {
-  // Scalar branch around the sqrt: most culled spheres pass for no lane of
-  // the wave in a given step, and then the whole body is skipped (the
-  // compiler would otherwise if-convert it and run the sqrt every time).
-  // sqrt_cr_normal also serves ss < 2^-96: see pass_body_r.
-  if (__builtin_amdgcn_ballot_w64(pass)) {
-    __asm__ volatile("; sphere passes for some lane");  // keeps the branch (no if-conversion)
-    if (pass) {
-      const float t = r - sqrt_cr_normal(ss);
-      L = max_nonneg(L, t);
-      dnew = k;
-    }
-  }
-}
-
 // One sphere test of the march (SphereWorld.cpp:365-369), exact: the pass
 // test is s < s_pass (see sfrt_world.cpp, pass_threshold) and sqrtf runs only
 // for a sphere that passes.
@@ -232,17 +191,7 @@ __device__ __forceinline__ float dist2(float px, float py, float pz, float cx, f
   return (ex * ex + ey * ey) + ez * ez;
 }
 
-__device__ __forceinline__ void sphere_step(float px, float py, float pz, float cx, float cy,
-                                            float cz, float r, float s_pass, int k, float& L,
-                                            int& dnew) {
-  const float ss = dist2(px, py, pz, cx, cy, cz);
-  pass_body(ss < s_pass, ss, r, k, L, dnew);
-}
-
-// R pixels per lane (an (8R)x8 tile per wave: columns c, c + 8, ...): the
-// wave-uniform work of a sphere visit -- record load, window bits, branch --
-// is shared by R rays, and each lane carries R independent dependency chains.
-// Same exact march as trace_tile_window, per ray.
+// Cone of an (8R)x8 tile whose lanes hold R rays each (columns c, c + 8, ...).
 template <int R>
 __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int tile_y,
                                             const float (&dx)[R], const float (&dy)[R],
@@ -302,15 +251,21 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
   }
 }
 
-// The n <= 64 march (SphereWorld.cpp:359-372), one wave per (8R)x8 tile.
-// Lane l holds R rays (columns c, c + 8, ...), so the wave-uniform half of a
-// sphere visit -- record load, window bits, branch -- is shared by R rays and
-// each lane carries R independent dependency chains.  Per wave: cull the
-// spheres against the tile cone (cull_window); a wave with <= kSlots culled
-// spheres holds them in SGPRs and tests each every step; otherwise each step
-// visits, in index order, the culled spheres whose march window meets the
-// along-ray distances [min over marching rays, max over the wave] (the low end
-// refreshed every second step: it only rises).  Then shade and store.
+// The march (SphereWorld.cpp:359-372), one wave per (8R)x8 tile.  Lane l holds
+// R rays (columns c, c + 8, ...), so the wave-uniform half of a sphere visit --
+// record load, window bits, branch -- is shared by R rays and each lane carries
+// R independent dependency chains.  Per wave: cull the spheres against the tile
+// cone (cull_window).  With n <= 64 (LIST = false, records in the kernel
+// arguments) lane l holds sphere l's march window and bit l of the culling mask
+// is sphere l; with n > 64 (LIST, records in device memory) the culled spheres
+// of every 64-sphere word are compacted, in index order, into lanes 0.. of a
+// culled list (cidx = the sphere index) -- a wave that culls more than 64
+// visits every sphere every step instead (exact; rare at the tile sizes used).
+// A wave with <= kSlots culled spheres holds them in SGPRs and tests each every
+// step; otherwise each step visits, in index order, the culled spheres whose
+// march window meets the along-ray distances [min over marching rays, max over
+// the wave] (the low end refreshed every second step: it only rises).  Then
+// shade and store.
 //
 // A stopped ray advances unmasked: it had no passing sphere at its position
 // (its last step visited every sphere that could pass for it) and never moves
@@ -319,7 +274,7 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
 // only reaches through -0 + d * l0 with d of negative sign, so d * (+0) = -0.
 // Edge lanes trace a clamped duplicate pixel (never stored) as the duplicate
 // it is, which keeps the tile cone tight.
-template <int R>
+template <int R, bool LIST>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
                                                     const SphereRec* __restrict__ sph) {
   const int lane = threadIdx.x & 63;
@@ -371,14 +326,49 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     for (int r = 0; r < R; r++) q |= __builtin_amdgcn_ballot_w64(mv[r] > 0.0f);
     return q != 0;
   };
-  const uint64_t all = f.n >= 64 ? ~0ull : ((1ull << f.n) - 1ull);
   const bool windowed = f.cull && l0 > 0.0f;
-  uint64_t m = all;
+  bool full = !windowed;  // visit every sphere every step
+  uint64_t m = 0;         // culled spheres (LIST: culled-list entries)
   float lo = -__builtin_inff(), hi = __builtin_inff();
+  int cidx = lane;        // sphere of culled-list entry `lane`
   if (windowed) {
     const Cone cone = tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
-    m = cull_window(f, sph, 0, cone, lo, hi);
+    if (!LIST) {
+      m = cull_window(f, sph, 0, cone, lo, hi);
+    } else {
+      __shared__ float s_list[3][64];  // compaction scratch: lo, hi, index
+      int count = 0;
+      const int nwords = (f.n + 63) >> 6;
+      for (int w = 0; w < nwords; w++) {
+        float wlo, whi;
+        const uint64_t mw = cull_window(f, sph, w * 64, cone, wlo, whi);
+        const int cw = __builtin_popcountll(mw);
+        if (count + cw > 64) {
+          full = true;
+          break;
+        }
+        if ((mw >> lane) & 1ull) {
+          const int dst = count + (int)__builtin_amdgcn_mbcnt_hi(
+                                      (uint32_t)(mw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mw, 0u));
+          s_list[0][dst] = wlo;
+          s_list[1][dst] = whi;
+          s_list[2][dst] = __int_as_float(w * 64 + lane);
+        }
+        count += cw;
+      }
+      __syncthreads();  // one wave: orders its own LDS writes before the reads
+      if (!full) {
+        m = count >= 64 ? ~0ull : ((1ull << count) - 1ull);
+        if (lane < count) {
+          lo = s_list[0][lane];
+          hi = s_list[1][lane];
+          cidx = __float_as_int(s_list[2][lane]);
+        }
+      }
+    }
   }
+  // sphere of culled entry e (wave-uniform)
+  auto entry = [&](int e) { return LIST ? __builtin_amdgcn_readlane(cidx, e) : e; };
 
   // pos += dir * L (SphereWorld.cpp:371) on every lane (see above)
   auto advance = [&](const float (&L)[R], const int (&dnew)[R]) {
@@ -399,54 +389,66 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     for (int r = 0; r < R; r++) ss[r] = dist2(px[r], py[r], pz[r], cx, cy, cz);
     pass_body_r<R>(ss, s_pass, rad, k, L, dnew);
   };
+  // Every sphere in index order (no culling: cull off, or past kCullSafeIterations steps).
+  auto visit_all = [&](float (&L)[R], int (&dnew)[R]) {
+    for (int k = 0; k < f.n; k++) {
+      const SphereRec& s = sph[k];
+      visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+    }
+  };
   int trips = 1;
-  if (windowed && __builtin_popcountll(m) <= kSlots) {
+#ifdef SFRT_SLOTS
+  constexpr int kSlotsR = SFRT_SLOTS;
+#else
+  constexpr int kSlotsR = kSlots;
+#endif
+  if (kSlotsR > 0 && !full && __builtin_popcountll(m) <= kSlotsR) {
+    constexpr int NS = kSlotsR > 0 ? kSlotsR : 1;
     // Few culled spheres: hold them in SGPR slots and test every one each step
     // (cheaper than maintaining the window).  Empty slots never pass.
-    float scx[kSlots], scy[kSlots], scz[kSlots], sr[kSlots], ssp[kSlots];
-    int sk[kSlots];
+    float scx[NS], scy[NS], scz[NS], sr[NS], ssp[NS];
+    int sk[NS];
     uint64_t mm = m;
 #pragma unroll
-    for (int q = 0; q < kSlots; q++) {
+    for (int q = 0; q < kSlotsR; q++) {
       scx[q] = scy[q] = scz[q] = sr[q] = ssp[q] = 0.0f;
       sk[q] = 0;
       if (mm) {
-        const int k = __builtin_ctzll(mm);
+        const int k = entry(__builtin_ctzll(mm));
         mm &= mm - 1;
         scx[q] = sph[k].cx; scy[q] = sph[k].cy; scz[q] = sph[k].cz;
         sr[q] = sph[k].r; ssp[q] = sph[k].s_pass;
         sk[q] = k;
       }
     }
-    uint64_t rest = 0;
     // single-exit loop (the march guard is part of the condition): a second
     // exit makes the compiler shuffle every loop-carried register each step
     for (; any_marching() && trips < kMaxIterations; ++trips) {
       if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
 #pragma unroll
-        for (int q = 0; q < kSlots; q++) ssp[q] = 0.0f;
-        rest = all;
+        for (int q = 0; q < kSlotsR; q++) ssp[q] = 0.0f;
+        full = true;
       }
       float L[R];
       int dnew[R];
 #pragma unroll
       for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
 #pragma unroll
-      for (int q = 0; q < kSlots; q++) visit(scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L, dnew);
-      for (uint64_t r2 = rest; r2; r2 &= r2 - 1) {
-        const int k = __builtin_ctzll(r2);
-        const SphereRec& s = sph[k];
-        visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
-      }
+      for (int q = 0; q < kSlotsR; q++) visit(scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L, dnew);
+      if (full) visit_all(L, dnew);
       advance(L, dnew);
     }
   } else {
-    bool full = !windowed;
     float tlo = 0.0f;
     for (; any_marching() && trips < kMaxIterations; ++trips) {
       if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
-      uint64_t win = all;
-      if (!full) {
+      float L[R];
+      int dnew[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
+      if (full) {
+        visit_all(L, dnew);
+      } else {
         // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32)
         uint32_t th = 0u;  // +0
 #pragma unroll
@@ -465,28 +467,26 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
           tlo = __uint_as_float(wave_min_u32(tl));
         }
         const float thi = __uint_as_float(wave_max_u32(th));
-        win = m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
-      }
-      float L[R];
-      int dnew[R];
-#pragma unroll
-      for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
-      // The visits, in index order, each issuing the next record's scalar loads before
-      // its own arithmetic (the loads' latency hides under the R rays' distance tests;
-      // kn = k for the last visit reloads a record already in the scalar cache).
-      if (win) {
-        uint64_t mm = win;
-        int k = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
-        for (;;) {
-          const int kn = mm ? __builtin_ctzll(mm) : k;
-          const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
-                      nsp = sph[kn].s_pass;
-          visit(cx, cy, cz, rad, sp, k, L, dnew);
-          if (!mm) break;
+        const uint64_t win =
+            m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
+        // The visits, in index order, each issuing the next record's scalar loads
+        // before its own arithmetic (the loads' latency hides under the R rays'
+        // distance tests; kn = k for the last visit reloads a record already in
+        // the scalar cache).
+        if (win) {
+          uint64_t mm = win;
+          int k = entry(__builtin_ctzll(mm));
           mm &= mm - 1;
-          k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
+          float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
+          for (;;) {
+            const int kn = mm ? entry(__builtin_ctzll(mm)) : k;
+            const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
+                        nsp = sph[kn].s_pass;
+            visit(cx, cy, cz, rad, sp, k, L, dnew);
+            if (!mm) break;
+            mm &= mm - 1;
+            k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
+          }
         }
       }
       advance(L, dnew);
@@ -504,108 +504,16 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   }
 }
 
+// n <= 64: the records travel in the kernel-argument segment.
 template <int R>
 __global__ __launch_bounds__(64) void k_trace_window_r(InlineArgs args) {
-  trace_tile_window_r<R>(args.f, args.s);
+  trace_tile_window_r<R, false>(args.f, args.s);
 }
 
-// n > 64 with the march window: per culling word, the lanes' (lo, hi) pairs
-// live in dynamic LDS ([wave][lo/hi][n rounded up to 64] floats).
-__device__ __forceinline__ void trace_tile_window_global(const FrameRec& f,
-                                                         const SphereRec* __restrict__ sph,
-                                                         float* __restrict__ s_win) {
-  __shared__ uint64_t s_mask[kWavesPerBlock][kMaskWords];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int tile = blockIdx.x * kWavesPerBlock + wave;
-  const int tile_y = tile / f.tiles_x;
-  const int tile_x = tile - tile_y * f.tiles_x;
-  if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
-  const int a = tile_x * kTile + (lane & 7);
-  const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
-  const int b_end = f.sub_row0 + f.sub_rows;
-  const bool valid = a < f.sub_w && b < b_end;
-  const int ac = a < f.sub_w ? a : f.sub_w - 1;
-  const int bc = b < b_end ? b : b_end - 1;
-  const int i = f.xstart + ac * f.xadd;
-  const int j = f.ystart + bc * f.yadd;
-
-  float dx, dy, dz;
-  primary_dir(f, i, j, dx, dy, dz);
-
-  const float l0 = f.first_l;
-  float px = f.cam[0] + dx * l0;
-  float py = f.cam[1] + dy * l0;
-  float pz = f.cam[2] + dz * l0;
-  int draw = f.first_draw;
-  float mv = (valid && l0 > 0.0f) ? 1.0f : 0.0f;
-  float tacc = l0;
-
-  const int nwords = (f.n + 63) >> 6;
-  float* const w_lo = s_win + (size_t)wave * 2 * nwords * 64;
-  float* const w_hi = w_lo + nwords * 64;
-  const bool any_march = __builtin_amdgcn_ballot_w64(mv > 0.0f) != 0;
-  const bool windowed = f.cull && any_march;
-  if (windowed) {
-    const Cone cone = tile_cone(f, tile_x, tile_y, dx, dy, dz);
-    for (int w = 0; w < nwords; w++) {
-      float lo, hi;
-      const uint64_t m = cull_window(f, sph, w * 64, cone, lo, hi);
-      if (lane == 0) s_mask[wave][w] = m;
-      w_lo[w * 64 + lane] = lo;
-      w_hi[w * 64 + lane] = hi;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  int trips = 1;
-  bool full = !windowed;
-  while (__builtin_amdgcn_ballot_w64(mv > 0.0f)) {
-    if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
-    float tlo = 0.0f, thi = 0.0f;
-    if (!full) {
-      tlo = __uint_as_float(wave_min_u32(__float_as_uint(mv > 0.0f ? tacc : __builtin_inff())));
-      thi = __uint_as_float(wave_max_u32(__float_as_uint(tacc)));
-    }
-    float L = 0.0f;
-    int dnew = draw;
-    for (int w = 0; w < nwords; w++) {
-      uint64_t win;
-      if (full) {
-        const int rem = f.n - w * 64;
-        win = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
-      } else {
-        win = uniform_u64(s_mask[wave][w]) &
-              __builtin_amdgcn_ballot_w64(w_lo[w * 64 + lane] < thi) &
-              __builtin_amdgcn_ballot_w64(w_hi[w * 64 + lane] > tlo);
-      }
-      for (; win; win &= win - 1) {
-        const int k = w * 64 + __builtin_ctzll(win);
-        const SphereRec& s = sph[k];
-        sphere_step(px, py, pz, s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
-      }
-    }
-    if (mv > 0.0f) {
-      px = px + dx * L;
-      py = py + dy * L;
-      pz = pz + dz * L;
-      draw = dnew;
-      mv = L;
-      tacc = tacc + L;
-    }
-    if (++trips >= kMaxIterations) {
-      if (mv > 0.0f) atomicOr(f.status, 1);
-      break;
-    }
-  }
-  if (!valid) return;
-  const SphereRec d = sph[draw];
-  const uint32_t rgba = shade(f, d, px, py, pz, nullptr);
-  f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
-}
-
-__global__ __launch_bounds__(256) void k_trace_global_window(FrameRec f) {
-  extern __shared__ float s_win[];
-  trace_tile_window_global(f, f.spheres, s_win);
+// n > 64: the records in device memory (f.spheres), the culled list per wave.
+template <int R>
+__global__ __launch_bounds__(64) void k_trace_window_list(FrameRec f) {
+  trace_tile_window_r<R, true>(f, f.spheres);
 }
 
 // Debug/parity kernel: one lane per listed pixel, full sphere list, float
@@ -664,13 +572,12 @@ static int ordered_rays(const FrameRec& f) {
 }
 
 // The one kernel table, shared by launch_trace and trace_tile_key: pixels per
-// lane of the n <= 64 kernel, or 0 for the n > 64 kernel.  Row-major launches
+// lane R (k_trace_window_r for n <= 64, k_trace_window_list above).  Row-major launches
 // use 16x8 tiles above kPairMinSpheres spheres and 8x8 tiles otherwise (their
 // tighter cones win there); ordered launches ordered_rays for any scene (1080p,
 // 10 spheres: 16x8 37.4 us against 42.0 with 8x8, which win only in row-major
 // order: 45.7 vs 48.5).  f.rays (SFRT_OPT_RAYS_PER_LANE) overrides the choice.
 static int trace_rays(const FrameRec& f, bool ordered) {
-  if (f.n > kInlineSpheres) return 0;
   if (f.rays >= 1 && f.rays <= 4) return f.rays;
   if (ordered) return ordered_rays(f);
   return f.n > kPairMinSpheres ? 2 : 1;
@@ -679,7 +586,6 @@ static int trace_rays(const FrameRec& f, bool ordered) {
 long long trace_tile_key(const FrameRec& f, long long* tiles) {
   *tiles = 0;
   const int rays = trace_rays(f, true);
-  if (rays == 0) return 0;
   const long long tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
   const long long tiles_y = (f.sub_rows + kTile - 1) / kTile;
   if (tiles_x <= 0 || tiles_y <= 0) return 0;
@@ -693,33 +599,35 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
   hipStream_t s = (hipStream_t)stream;
   const bool ordered = f.tile_cost != nullptr;  // linked into the tile-order chain
   const int rays = trace_rays(f, ordered);
-  if (rays > 0) {
+  FrameRec g = f;
+  g.tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
+  const long long tiles = tiles_y * g.tiles_x;
+  long long key_tiles = 0;
+  if (!ordered || trace_tile_key(f, &key_tiles) == 0 || key_tiles != tiles) {
+    g.tile_order = nullptr; g.tile_cost = nullptr; g.prev_cost = nullptr;
+  }
+  // one wave per workgroup (a finished wave's slot refills at once), plus the
+  // tile-order sorter (sfrt_trace.h FrameRec)
+  const long long blocks = tiles + (g.prev_cost ? 1 : 0);
+  if (blocks > 0x7fffffffLL) return -1;
+  const dim3 gr((unsigned)blocks), b(64);
+  if (f.n <= kInlineSpheres) {
     InlineArgs args;
-    args.f = f;
-    args.f.tiles_x = (f.sub_w + rays * kTile - 1) / (rays * kTile);
+    args.f = g;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
-    const long long tiles = tiles_y * args.f.tiles_x;
-    long long key_tiles = 0;
-    if (!ordered || trace_tile_key(f, &key_tiles) == 0 || key_tiles != tiles) {
-      args.f.tile_order = nullptr; args.f.tile_cost = nullptr; args.f.prev_cost = nullptr;
-    }
-    // one wave per workgroup (a finished wave's slot refills at once), plus the
-    // tile-order sorter (sfrt_trace.h FrameRec)
-    const long long blocks = tiles + (args.f.prev_cost ? 1 : 0);
-    if (blocks > 0x7fffffffLL) return -1;
-    const dim3 g((unsigned)blocks), b(64);
     switch (rays) {
-      case 1: hipLaunchKernelGGL(k_trace_window_r<1>, g, b, 0, s, args); break;
-      case 2: hipLaunchKernelGGL(k_trace_window_r<2>, g, b, 0, s, args); break;
-      case 3: hipLaunchKernelGGL(k_trace_window_r<3>, g, b, 0, s, args); break;
-      default: hipLaunchKernelGGL(k_trace_window_r<4>, g, b, 0, s, args); break;
+      case 1: hipLaunchKernelGGL(k_trace_window_r<1>, gr, b, 0, s, args); break;
+      case 2: hipLaunchKernelGGL(k_trace_window_r<2>, gr, b, 0, s, args); break;
+      case 3: hipLaunchKernelGGL(k_trace_window_r<3>, gr, b, 0, s, args); break;
+      default: hipLaunchKernelGGL(k_trace_window_r<4>, gr, b, 0, s, args); break;
     }
   } else {
-    const long long tiles = tiles_y * f.tiles_x;
-    const long long blocks = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (blocks > 0x7fffffffLL) return -1;
-    const size_t lds = (size_t)kWavesPerBlock * 2 * (size_t)((f.n + 63) / 64) * 64 * sizeof(float);
-    hipLaunchKernelGGL(k_trace_global_window, dim3((unsigned)blocks), dim3(256), lds, s, f);
+    switch (rays) {
+      case 1: hipLaunchKernelGGL(k_trace_window_list<1>, gr, b, 0, s, g); break;
+      case 2: hipLaunchKernelGGL(k_trace_window_list<2>, gr, b, 0, s, g); break;
+      case 3: hipLaunchKernelGGL(k_trace_window_list<3>, gr, b, 0, s, g); break;
+      default: hipLaunchKernelGGL(k_trace_window_list<4>, gr, b, 0, s, g); break;
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -97,16 +97,17 @@ def test_cull_on_off_identical(world, floor):
 
 @pytest.mark.parametrize("rays", [1, 2, 3, 4])
 def test_tile_shapes_identical(world, floor, rays):
-    """Every shipped tile shape of the <= 64-sphere kernel ((8R)x8 tiles, R pixels per lane,
-    forced with SFRT_OPT_RAYS_PER_LANE) produces the default kernel's bytes, in row-major
-    order (update_image) and in the adaptive tile order (three render_band frames back to
-    back), on ragged frames (64 spheres, 4K, rotated pose; random poses of three scenes)."""
+    """Every shipped tile shape ((8R)x8 tiles, R pixels per lane, forced with
+    SFRT_OPT_RAYS_PER_LANE; the kernel-argument kernel up to 64 spheres, the culled-list
+    kernel above) produces the default kernel's bytes, in row-major order (update_image) and
+    in the adaptive tile order (three render_band frames back to back), on ragged frames
+    (64 spheres, 4K, rotated pose; random poses of four scenes, 256 spheres among them)."""
     import sfrt
     import torch
     cases = [(scenes.lcg64(), (1.1, -0.2), 3840, 2160)]
     rng = np.random.default_rng(rays)
-    for sc in (scenes.lcg64(), scenes.default10(), scenes.one_sphere()):
-        for _ in range(4):
+    for sc in (scenes.lcg64(), scenes.default10(), scenes.one_sphere(), scenes.lcg256()):
+        for _ in range(4 if sc.name != "lcg256" else 2):
             cases.append((sc, (float(rng.uniform(0, 6.3)), float(rng.uniform(-0.6, 0.6))), 1000, 563))
     stream = torch.cuda.Stream()
     for sc, pose, width, height in cases:
@@ -218,8 +219,31 @@ def test_camera_outside_every_sphere(world, floor):
     assert diff_report(got, want, 160) == ""
 
 
+@pytest.mark.parametrize("pose", [(0.0, 0.0), (1.1, -0.2)])
+def test_lcg256_ordered_frames_match_oracle(world, floor, pose):
+    """256 spheres (the culled-list kernel, 32x8 tiles at 1600 x 1200 in the adaptive tile
+    order, four frames back to back) against the oracle."""
+    import torch
+    width, height = 1600, 1200
+    scene = scenes.lcg256().posed(*pose)
+    world.set_scene(scene, width, height)
+    want = oracle_for(scene, width, height, floor).render(host_threads())
+    stream = torch.cuda.Stream()
+    bufs = []
+    with torch.cuda.stream(stream):
+        for _ in range(4):
+            b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+            bufs.append(b)
+    world.check(stream.cuda_stream)
+    torch.cuda.synchronize()
+    for k, b in enumerate(bufs):
+        assert diff_report(b.cpu().numpy().ravel(), want, width) == "", (pose, k)
+    assert diff_report(world.render(), want, width) == "", pose
+
+
 def test_many_spheres_global_path(world, floor):
-    """n > 64 takes the device-buffer kernel (multi-word culling masks)."""
+    """n > 64 takes the device-buffer kernel (culled list over multi-word masks)."""
     spheres = scenes.sort_spheres(scenes.lcg_spheres(count=199, seed=777))
     scene = scenes.Scene("lcg200", spheres).posed(0.4, -0.1)
     world.set_scene(scene, 640, 360)

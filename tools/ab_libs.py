@@ -1,6 +1,7 @@
 """Build-flag A/B of libsfrt.so builds, interleaved across processes, bytes checked.
 
-    python tools/ab_libs.py --libs a.so,b.so [--rounds 3] [--reps 40] [--cases 4k,4k_rot,...]
+    python tools/ab_libs.py --libs a.so,b.so,a.so@3 [--rounds 3] [--reps 40] [--cases 4k,4k_rot,...]
+(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE)
 
 Each round starts one process per library (SFRT_LIB=<lib>, the same sfrt.py), which
 times every case with HIP events (median kernel time, event-pair overhead subtracted;
@@ -26,7 +27,7 @@ CASES = {
 }
 
 
-def child(cases, reps):
+def child(cases, reps, rays):
     sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -38,6 +39,7 @@ def child(cases, reps):
     torch.cuda.set_stream(stream)
     w = sfrt.World(0)
     w.load_texture(*scenes.load_floor())
+    w.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
     pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
              for _ in range(64)]
     for a, b in pairs:
@@ -78,19 +80,21 @@ def main():
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--cases", default="4k,4k_rot,4k_turn,8k,1080")
     ap.add_argument("--child", action="store_true")
+    ap.add_argument("--rays", type=int, default=0, help="(child) SFRT_OPT_RAYS_PER_LANE")
     a = ap.parse_args()
     cases = a.cases.split(",")
     if a.child:
-        child(cases, a.reps)
+        child(cases, a.reps, a.rays)
         return
     libs = a.libs.split(",")
     res = {lib: {c: [] for c in cases} for lib in libs}
     hashes = {}
     for rnd in range(a.rounds):
-        for lib in libs:
-            env = dict(os.environ, SFRT_LIB=os.path.abspath(lib))
+        for lib in libs:  # "path" or "path@R" (R = SFRT_OPT_RAYS_PER_LANE)
+            path, _, rays = lib.partition("@")
+            env = dict(os.environ, SFRT_LIB=os.path.abspath(path))
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
-                                "--cases", a.cases, "--reps", str(a.reps)],
+                                "--cases", a.cases, "--reps", str(a.reps), "--rays", rays or "0"],
                                capture_output=True, text=True, env=env, timeout=600)
             line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")]
             if r.returncode != 0 or not line:
