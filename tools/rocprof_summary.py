@@ -26,10 +26,18 @@ import re
 
 
 def pixels_per_thread(kernel_name: str) -> int:
-    """Pixels one work-item writes: R for k_trace_window_r<R> (round 1: <SLOTS, R, ...>), else 1."""
-    m = re.search(r"k_trace_window_r<\s*(\d+)\s*>", kernel_name) or \
+    """Pixels one work-item writes: R for k_trace_window_r<R> / k_trace_window_list<R>
+    (round 1: k_trace_window_r<SLOTS, R, ...>), else 1."""
+    m = re.search(r"k_trace_window_(?:r|list)<\s*(\d+)\s*>", kernel_name) or \
         re.search(r"k_trace_window_r<\s*\d+\s*,\s*(\d+)", kernel_name)
     return int(m.group(1)) if m else 1
+
+
+def launch_key(kernel_name: str, grid: int) -> str:
+    """Pixels per launch; the n > 64 culled-list kernel's launches get a "list:" prefix so
+    that they never mix with the n <= 64 kernel's at the same frame size."""
+    px = grid * pixels_per_thread(kernel_name)
+    return f"list:{px}" if "k_trace_window_list" in kernel_name else str(px)
 
 
 def rows(d, name):
@@ -65,22 +73,22 @@ def main():
         acc = collections.defaultdict(list)
         for r in rows(d, "counter_collection"):
             if a.kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                px = int(r["Grid_Size"]) * pixels_per_thread(r["Kernel_Name"])
-                acc[px].append(float(r["Counter_Value"]) * 1024.0)
+                acc[launch_key(r["Kernel_Name"], int(r["Grid_Size"]))].append(
+                    float(r["Counter_Value"]) * 1024.0)
         for grid, v in acc.items():
             traffic.setdefault(str(grid), {})[counter] = sum(v) / len(v)
     for sq_dir in a.sq:
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in rows(sq_dir, "counter_collection"):
             if a.kernel in r["Kernel_Name"]:
-                px = int(r["Grid_Size"]) * pixels_per_thread(r["Kernel_Name"])
-                acc[px][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                acc[launch_key(r["Kernel_Name"], int(r["Grid_Size"]))][r["Counter_Name"]].append(
+                    float(r["Counter_Value"]))
         for grid, cs in acc.items():
             for c, v in cs.items():
                 traffic.setdefault(str(grid), {})[c] = sum(v) / len(v)
     for g, t in traffic.items():
         t["hbm_bytes_per_launch"] = 2.0 * t.get("FETCH_SIZE", 0.0) + t.get("WRITE_SIZE", 0.0)
-        t["algorithmic_bytes_per_launch"] = 4.0 * int(g)
+        t["algorithmic_bytes_per_launch"] = 4.0 * int(g.split(":")[-1])
     with open(os.path.join(a.out, f"{a.tag}_traffic.json"), "w") as f:
         json.dump({"note": __doc__.split("Writes")[0].strip(), "kernel": a.kernel,
                    "per_launch_pixels": traffic}, f, indent=1)
