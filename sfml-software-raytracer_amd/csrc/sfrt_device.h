@@ -168,8 +168,13 @@ __device__ __forceinline__ uint32_t tile_bucket(uint32_t steps) {
 // counting and ranking need no atomics; the exclusive scan runs bucket-major
 // over (bucket, lane), which keeps chunk order -- tile order -- within a bucket.
 // (Per-lane counters: LDS atomics without conflicts.)
+// dilate (a moving camera): tile t is ranked by the longest of tiles t - 1, t,
+// t + 1 (its row neighbours; across a row end the neighbour is the other row's
+// end tile, a harmless over-estimate): content that a turning camera moves by
+// less than a tile between the recorded frame and the one the order serves
+// stays inside that window, so a tile that turns long is not left for the end.
 __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int n,
-                                           uint32_t* __restrict__ order) {
+                                           uint32_t* __restrict__ order, bool dilate = false) {
   __shared__ uint32_t cnt[kTileBuckets][64];
   const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -181,21 +186,46 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
   // the n % 16 tail tiles go to the last lane's chunk end (after vector nvec - 1)
   const bool tail = lane == 63;
   const uint4* __restrict__ cv = reinterpret_cast<const uint4*>(cost);
+  auto at = [&](int t) { return (uint32_t)cost[t < 0 ? 0 : t >= n ? n - 1 : t]; };
   auto pass = [&](auto&& one) {
+    uint32_t prev = dilate && v0 < v1 ? at(16 * v0 - 1) : 0u;  // bucket of the tile before
     for (int v = v0; v < v1; v += 8) {
       uint4 q[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) q[u] = v + u < v1 ? cv[v + u] : make_uint4(0, 0, 0, 0);
+      const uint32_t after = dilate ? at(16 * (v + 8 < v1 ? v + 8 : v1)) : 0u;
 #pragma unroll
       for (int u = 0; u < 8; u++) {
         if (v + u >= v1) break;
         const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+        if (!dilate) {
 #pragma unroll
-        for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
+          for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
+          continue;
+        }
+        const uint32_t nxt = u + 1 < 8 && v + u + 1 < v1 ? (q[u + 1].x & 0xffu) : after;
+        uint32_t cur = w[0] & 0xffu;
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+          const uint32_t right = e < 15 ? (w[(e + 1) >> 2] >> (8 * ((e + 1) & 3))) & 0xffu : nxt;
+          uint32_t m = prev < cur ? prev : cur;  // bucket 0 = longest: the minimum
+          m = right < m ? right : m;
+          one(m, (v + u) * 16 + e);
+          prev = cur;
+          cur = right;
+        }
       }
     }
     if (tail)
-      for (int t = nvec * 16; t < n; t++) one((uint32_t)cost[t], t);
+      for (int t = nvec * 16; t < n; t++) {
+        uint32_t m = at(t);
+        if (dilate) {
+          const uint32_t l = at(t - 1), r = at(t + 1);
+          m = l < m ? l : m;
+          m = r < m ? r : m;
+        }
+        one(m, t);
+      }
   };
   // LDS atomics on the lane's own counters: no conflicts, and the count pass's
   // need no return (a plain read-modify-write would wait on every read)

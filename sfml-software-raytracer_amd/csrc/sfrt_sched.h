@@ -34,6 +34,7 @@ struct TileSched {
   bool sorted_prev = false;      // launch k-1 sorted launch k-2's tiles into order[k % 2]
   long long pending_key = 0;     // begin() -> end(): the launch being queued
   bool pending_sorted = false;
+  bool committed = false;        // the last end() advanced the chain
   hipStream_t last_stream = nullptr;
   bool have_last = false;
 
@@ -90,10 +91,12 @@ struct TileSched {
   // never written, so no later launch may sort it or read an order built from it.
   hipError_t end(const TileSchedPtrs& p, hipStream_t s, bool queued = true) {
     if (!p.tile_cost) return hipSuccess;
+    committed = false;
     if (!queued) {
       reset();
       return hipSuccess;
     }
+    committed = pending_key != 0;
     if (pending_key) {
       sorted_prev = pending_sorted;
       key_prev = pending_key;

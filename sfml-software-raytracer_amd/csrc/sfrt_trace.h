@@ -65,6 +65,9 @@ struct FrameRec {
   uint8_t* tile_cost;
   const uint8_t* prev_cost;
   uint32_t* next_order;
+  // The camera moved since the launch whose classes the sorter ranks: rank each
+  // tile by the longest of it and its row neighbours (sfrt_device.h sort_tiles).
+  int order_dilate;
 };
 
 // Kernel argument for n <= kInlineSpheres: frame + spheres in the kernarg segment.

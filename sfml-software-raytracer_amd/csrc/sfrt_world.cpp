@@ -27,6 +27,7 @@
 
 #pragma clang fp contract(off)
 
+
 namespace {
 
 constexpr float kPI = 3.1415926535f;  // SphereWorld.h:6
@@ -332,6 +333,9 @@ struct sfrt_world {
     f.tile_cost = p.tile_cost;
     f.prev_cost = p.prev_cost;
     f.next_order = p.next_order;
+    // a moving camera: the recorded classes are a frame or two off
+    f.order_dilate = p.prev_cost && chain_last.valid &&
+                     std::memcmp(&chain_last.cam, &cam, sizeof cam) != 0;
     return SFRT_OK;
   }
 
@@ -340,8 +344,22 @@ struct sfrt_world {
     sfrt::TileSchedPtrs p;
     p.tile_cost = f.tile_cost;
     HIP_TRY(sched.end(p, s, queued));
-    return queued ? SFRT_OK : SFRT_E_HIP;
+    if (!queued) {
+      chain_last.valid = false;
+      return SFRT_E_HIP;
+    }
+    if (sched.committed) chain_last = ChainCam{true, cam, f.sub_row0};
+    return SFRT_OK;
   }
+
+  // The camera of the last launch that joined the tile-order chain: its costs are the
+  // ones the next launch's sorter ranks.
+  struct ChainCam {
+    bool valid = false;
+    sfrt_camera cam{};
+    int sub_row0 = 0;
+  };
+  ChainCam chain_last;
 
   int read_status(hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));

@@ -283,7 +283,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   int slot = (int)blockIdx.x;
   if (f.prev_cost) {
     if (blockIdx.x == 0) {
-      sort_tiles(f.prev_cost, ntiles, f.next_order);
+      sort_tiles(f.prev_cost, ntiles, f.next_order, f.order_dilate != 0);
       return;
     }
     slot -= 1;
@@ -296,6 +296,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   const int tile_y = tile / f.tiles_x;  // f.tiles_x = ceil(sub_w / (8 R)) for this kernel
   const int tile_x = tile - tile_y * f.tiles_x;
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
+#if SFRT_EXP & 16  // diagnostic build: per-tile wall-clock start/end (wrong bytes)
+  const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
   const int b_end = f.sub_row0 + f.sub_rows;
   const int bc = b < b_end ? b : b_end - 1;
@@ -397,6 +400,21 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
   };
   int trips = 1;
+  auto boost = [](int t) {
+#if SFRT_EXP & 1
+    if (t == 24) __builtin_amdgcn_s_setprio(1);
+    if (t == 40) __builtin_amdgcn_s_setprio(2);
+    if (t == 56) __builtin_amdgcn_s_setprio(3);
+#elif SFRT_EXP & 2
+    if (t == 32) __builtin_amdgcn_s_setprio(3);
+#elif SFRT_EXP & 4
+    if (t == 16) __builtin_amdgcn_s_setprio(1);
+    if (t == 24) __builtin_amdgcn_s_setprio(2);
+    if (t == 32) __builtin_amdgcn_s_setprio(3);
+#else
+    (void)t;
+#endif
+  };
 #ifdef SFRT_SLOTS
   constexpr int kSlotsR = SFRT_SLOTS;
 #else
@@ -424,6 +442,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     // single-exit loop (the march guard is part of the condition): a second
     // exit makes the compiler shuffle every loop-carried register each step
     for (; any_marching() && trips < kMaxIterations; ++trips) {
+      boost(trips);
       if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
 #pragma unroll
         for (int q = 0; q < kSlotsR; q++) ssp[q] = 0.0f;
@@ -441,6 +460,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   } else {
     float tlo = 0.0f;
     for (; any_marching() && trips < kMaxIterations; ++trips) {
+      boost(trips);
       if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
       float L[R];
       int dnew[R];
@@ -497,11 +517,24 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (valid[r]) {
+#if SFRT_EXP & 64  // timing probe only (wrong bytes): the march without the shading tail
+      f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] =
+          __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^ __float_as_uint(pz[r]) ^ (uint32_t)draw[r];
+      continue;
+#endif
       const SphereRec d = sph[draw[r]];
       const uint32_t rgba = shade(f, d, px[r], py[r], pz[r], nullptr);
       f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] = rgba;
     }
   }
+#if SFRT_EXP & 16
+  const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
+  if (lane < 4 && valid[0]) {
+    const uint32_t v = lane == 0 ? (uint32_t)dbg_t0 : lane == 1 ? (uint32_t)dbg_t1
+                     : lane == 2 ? (uint32_t)trips : (uint32_t)slot;
+    f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[0]] = v;
+  }
+#endif
 }
 
 // n <= 64: the records travel in the kernel-argument segment.

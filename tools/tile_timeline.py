@@ -1,0 +1,55 @@
+"""Diagnostic: per-tile wall-clock start/end of the sphere kernel (a build with
+-DSFRT_EXP=16 writes them into pixels 0-3 of each tile's first row; wrong image bytes).
+    SFRT_LIB=sfml-software-raytracer_amd/build_x16/libsfrt.so python tools/tile_timeline.py
+Prints the kernel's span, the distribution of tile durations, and when the longest
+tiles start and end, for a static and a turning camera."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import scenes  # noqa: E402
+import sfrt  # noqa: E402
+
+
+def main():
+    W, H, R = 3840, 2160, 4
+    stream = torch.cuda.Stream()
+    w = sfrt.World(0)
+    w.load_texture(*scenes.load_floor())
+    sc = scenes.lcg64()
+    out = {}
+    for name, turn, order in (("static", False, 1), ("turning", True, 1), ("static_rowmajor", False, 0)):
+        w.set_scene(sc, W, H)
+        w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+        buf = torch.zeros(H, W * 4, dtype=torch.uint8, device="cuda")
+        for k in range(300):
+            if turn:
+                w.set_camera(sc.cam_pos, 0.004 * k, 0.0)
+            w.render_band(buf.data_ptr(), W * 4, 0, H, stream.cuda_stream)
+        torch.cuda.synchronize()
+        px = buf.cpu().numpy().view(np.uint32).reshape(H, W)
+        tiles = px[0::8, :].reshape(H // 8, W // (8 * R), 8 * R)[:, :, :4].reshape(-1, 4).astype(np.int64)
+        t0, t1, trips, slot = tiles[:, 0], tiles[:, 1], tiles[:, 2], tiles[:, 3]
+        base = t0.min()
+        t0 = (t0 - base) * 10  # ns (100 MHz)
+        t1 = (t1 - base) * 10
+        dur = t1 - t0
+        top = np.argsort(-dur)[:10]
+        out[name] = {
+            "span_us": round(float(t1.max()) / 1e3, 1),
+            "last_start_us": round(float(t0.max()) / 1e3, 1),
+            "dur_us_p50_p90_p99_max": [round(float(np.percentile(dur, q)) / 1e3, 1) for q in (50, 90, 99, 100)],
+            "longest": [{"trips": int(trips[i]), "start_us": round(t0[i] / 1e3, 1), "end_us": round(t1[i] / 1e3, 1),
+                         "slot": int(slot[i])} for i in top],
+            "sum_dur_over_8192_slots_us": round(float(dur.sum()) / 8192 / 1e3, 1),
+        }
+        print(name, json.dumps(out[name]), flush=True)
+    w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+
+
+if __name__ == "__main__":
+    main()
