@@ -25,8 +25,11 @@
 
 #pragma clang fp contract(off)
 
+// Diagnostic builds only (tools/ab_libs.py, tools/tile_timeline.py), never the shipped
+// library: -DSFRT_EXP=16 writes per-tile wall-clock start/end into each tile's first
+// pixels, -DSFRT_EXP=64 skips the shading tail (timing probes; both write wrong bytes).
 #ifndef SFRT_EXP
-#define SFRT_EXP 0  // build-flag A/B knobs (tools/ab_libs.py); 0 = the shipped kernel
+#define SFRT_EXP 0
 #endif
 
 namespace sfrt {
@@ -400,21 +403,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
   };
   int trips = 1;
-  auto boost = [](int t) {
-#if SFRT_EXP & 1
-    if (t == 24) __builtin_amdgcn_s_setprio(1);
-    if (t == 40) __builtin_amdgcn_s_setprio(2);
-    if (t == 56) __builtin_amdgcn_s_setprio(3);
-#elif SFRT_EXP & 2
-    if (t == 32) __builtin_amdgcn_s_setprio(3);
-#elif SFRT_EXP & 4
-    if (t == 16) __builtin_amdgcn_s_setprio(1);
-    if (t == 24) __builtin_amdgcn_s_setprio(2);
-    if (t == 32) __builtin_amdgcn_s_setprio(3);
-#else
-    (void)t;
-#endif
-  };
+
 #ifdef SFRT_SLOTS
   constexpr int kSlotsR = SFRT_SLOTS;
 #else
@@ -442,7 +431,6 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     // single-exit loop (the march guard is part of the condition): a second
     // exit makes the compiler shuffle every loop-carried register each step
     for (; any_marching() && trips < kMaxIterations; ++trips) {
-      boost(trips);
       if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
 #pragma unroll
         for (int q = 0; q < kSlotsR; q++) ssp[q] = 0.0f;
@@ -460,7 +448,6 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   } else {
     float tlo = 0.0f;
     for (; any_marching() && trips < kMaxIterations; ++trips) {
-      boost(trips);
       if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
       float L[R];
       int dnew[R];

@@ -1,8 +1,9 @@
-"""Model of the sphere kernel's march visits: for random 16x8 tiles of the 4K
+"""Model of the sphere kernel's march visits: for random 32x8 tiles of the 4K
 64-sphere frame, simulate the march in numpy float32 (approximate pass threshold; counts only)
-and count per step the spheres the kernel visits (cull cone + march window, low end every 2nd
-step, SGPR-slot waves visit all their culled spheres) against those that pass for some lane.
-    python tools/visit_model.py [rotation hrotation]
+and count per step the spheres the kernel visits (cull cone + march window with the half-width
+sqrt(rr^2 - dmin^2), low end every 2nd step, SGPR-slot waves visit all their culled spheres)
+against those that pass for some lane.
+    python tools/visit_model.py [rotation hrotation] [--round1-window]
 """
 import os, sys
 import numpy as np
@@ -10,7 +11,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import scenes
 f32 = np.float32
 W, H = 3840, 2160
-pose = tuple(float(x) for x in sys.argv[1:3]) if len(sys.argv) > 2 else (0.0, 0.0)
+args = [a for a in sys.argv[1:] if not a.startswith('--')]
+ROUND1 = '--round1-window' in sys.argv
+pose = tuple(float(x) for x in args[:2]) if len(args) > 1 else (0.0, 0.0)
 sc = scenes.lcg64().posed(*pose)
 S = sc.spheres.astype(f32); n = len(S)
 cam = np.array(sc.cam_pos, f32)
@@ -35,7 +38,8 @@ spass = (rs - f32(0.01))**2  # approx threshold
 reach = max(np.linalg.norm(cam), (np.linalg.norm(cs, axis=1) + rs).max())
 margin = f32(1e-3 * reach + 1e-4)
 rng = np.random.default_rng(0)
-TX, TY = 16, 8
+TX, TY = 32, 8
+SLOTS = 2
 ntiles = 3000
 tot_steps = tot_win = tot_min = tot_slot = 0; tot_win_onlymin=0
 for t in range(ntiles):
@@ -61,9 +65,14 @@ for t in range(ntiles):
     sa = perp * cos_t - tt * sin_t; sb = perp * cos_t + tt * sin_t
     inc = (wl <= rr) | (side & (sa <= rr))
     upb = np.where(sa >= 0, tt*cos_t + perp*sin_t, wl); dn = np.where(sb >= 0, tt*cos_t - perp*sin_t, -wl)
-    lo = dn - (rr + margin); hi = upb + (rr + margin)
+    if ROUND1:
+        h = rr
+    else:
+        dmin = np.maximum(0.0, np.minimum(sa, sb) - 4e-6 * wl)
+        h = np.sqrt(np.maximum(0.0, (rr - dmin) * (rr + dmin))) * 1.00001
+    lo = dn - (h + margin); hi = upb + (h + margin)
     m = inc.copy()
-    slots = m.sum() <= 4
+    slots = m.sum() <= SLOTS
     trips = 1; tlo = 0.0
     while mv.any():
         if trips % 2 == 1: tlo = tacc[mv].min()
