@@ -63,6 +63,37 @@ __device__ __forceinline__ float sqrt_cr_normal(float x) {
   return q;
 }
 
+// a / b, correctly rounded, for operands that need none of the hardware division's
+// range handling.  hipcc lowers a binary32 `a / b` on gfx950 to
+//   d = v_div_scale(b, b, a); y0 = v_rcp(d); y = fma(fma(-d, y0, 1), y0, y0);
+//   n = v_div_scale(a, b, a); q = n*y; q = fma(fma(-d, q, n), y, q);
+//   v_div_fixup(v_div_fmas(fma(-d, q, n), y, q), b, a)
+// (11 VALU).  v_div_scale returns its operand unchanged and clears VCC -- so
+// v_div_fmas is a plain fma -- unless a or b is zero, denormal, inf or NaN, 1/b
+// or a/b is denormal, |a| < 2^-103 or a's exponent exceeds b's by 96 or more;
+// v_div_fixup returns the quotient unchanged when it is finite, normal and
+// neither operand is special.  For finite normal a, b with a/b normal, and
+// |b| < 2^126, all of that holds, and div_seed(b) + div_inrange(a, b, y) run
+// the same operations on the same values (2 + 5 VALU, the seed shared by every
+// division by b).  Also exact for a = +0 with b > 0 (every step yields +0).
+// Checked against `/` on gfx950 (tests/native/div_check.hip, classes 3-4).
+__device__ __forceinline__ float div_seed(float b) {
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  return __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+}
+__device__ __forceinline__ float div_inrange(float a, float b, float y) {
+  float q = a * y;
+  q = __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+  return __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+}
+__device__ __forceinline__ float div_inrange(float a, float b) { return div_inrange(a, b, div_seed(b)); }
+
+// |v| in [2^-40, 2^40) (so finite, non-zero, normal): two quotients of such
+// values are normal and every precondition of div_inrange holds.
+__device__ __forceinline__ uint32_t div_operand_ok(float v) {  // 0 / 1, combined with &
+  return (sfrt_math::f2u(v) & 0x7fffffffu) - 0x2b800000u < 0x53800000u - 0x2b800000u;
+}
+
 // atan2f(y, x), bit for bit sfrt_math::atan2f (= glibc's e_atan2f.c), with a
 // cheaper path for the waves the renderers produce.  When every lane of the
 // wave has finite non-zero x and y and |y/x| in [2^-29, 2^25), no special case
@@ -77,11 +108,12 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
   using sfrt_math::f2u;
   using sfrt_math::u2f;
   const uint32_t hx = f2u(x), hy = f2u(y);
-  const uint32_t ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
-  const float q = y / x;
+  // |x|, |y| in [2^-40, 2^40): y / x through div_inrange (a wave with other operands,
+  // all rare, takes the general code, like one with |y/x| outside [2^-29, 2^25))
+  const float q = div_inrange(y, x);
   const uint32_t iq = f2u(q) & 0x7fffffffu;
-  const bool general = (ix - 1u < 0x7f7fffffu) & (iy - 1u < 0x7f7fffffu) &
-                       (iq - 0x31000000u < 0x4c000000u - 0x31000000u);
+  const bool general = div_operand_ok(x) & div_operand_ok(y) &
+                       (uint32_t)(iq - 0x31000000u < 0x4c000000u - 0x31000000u);
   if (__builtin_amdgcn_ballot_w64(!general)) return sfrt_math::atan2f(y, x);
   const float a = u2f(iq);
   const int id = iq < 0x3ee00000u ? -1
@@ -89,6 +121,9 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
                : iq < 0x3f980000u ? 1
                : iq < 0x401c0000u ? 2
                : 3;
+  // The reduction divisions below use div_inrange: a in [2^-29, 2^25) makes every
+  // denominator lie in [1, 1.5 * 2^25 + 1] and every numerator +0 (a = 0.5, 1, 1.5)
+  // or of magnitude >= 2^-29 (a multiple of a's ulp, or a itself over 1).
   // s_atanf.c tail for the reduced argument xr: (s1 + s2) * xr and the final sum
   auto poly = [](float xr) {
     const float z = xr * xr;
@@ -115,16 +150,16 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
     } else {
       float xr, hi, lo;
       if (id0 == 0) {
-        xr = ((a + a) - 1.0f) / (a + 2.0f);
+        xr = div_inrange((a + a) - 1.0f, a + 2.0f);
         hi = u2f(0x3eed6338u); lo = u2f(0x31ac3769u);
       } else if (id0 == 1) {
-        xr = (a - 1.0f) / (a + 1.0f);
+        xr = div_inrange(a - 1.0f, a + 1.0f);
         hi = u2f(0x3f490fdau); lo = u2f(0x33222168u);
       } else if (id0 == 2) {
-        xr = (a - 1.5f) / (a * 1.5f + 1.0f);
+        xr = div_inrange(a - 1.5f, a * 1.5f + 1.0f);
         hi = u2f(0x3f7b985eu); lo = u2f(0x33140fb4u);
       } else {
-        xr = -1.0f / a;
+        xr = div_inrange(-1.0f, a);
         hi = u2f(0x3fc90fdau); lo = u2f(0x33a22168u);
       }
       zr = hi - ((poly(xr) - lo) - xr);
@@ -135,7 +170,7 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
     if (id == 1) { num = a - 1.0f; den = a + 1.0f; }
     if (id == 2) { num = a - 1.5f; den = a * 1.5f + 1.0f; }
     if (id == 3) { num = -1.0f; den = a; }
-    const float xr = num / den;
+    const float xr = div_inrange(num, den);
     const float xs = poly(xr);
     float hi = u2f(0x3fc90fdau), lo = u2f(0x33a22168u);
     if (id == 0) { hi = u2f(0x3eed6338u); lo = u2f(0x31ac3769u); }
@@ -187,15 +222,18 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
   const bool tail = lane == 63;
   const uint4* __restrict__ cv = reinterpret_cast<const uint4*>(cost);
   auto at = [&](int t) { return (uint32_t)cost[t < 0 ? 0 : t >= n ? n - 1 : t]; };
-  auto pass = [&](auto&& one) {
+  // D loads in flight: 8, or 4 when dilating (its three bytes per tile would otherwise
+  // lift the kernel past 64 VGPRs -- one wave per SIMD fewer for every render wave)
+  auto pass = [&](auto d_tag, auto&& one) {
+    constexpr int D = decltype(d_tag)::value;
     uint32_t prev = dilate && v0 < v1 ? at(16 * v0 - 1) : 0u;  // bucket of the tile before
-    for (int v = v0; v < v1; v += 8) {
-      uint4 q[8];
+    for (int v = v0; v < v1; v += D) {
+      uint4 q[D];
 #pragma unroll
-      for (int u = 0; u < 8; u++) q[u] = v + u < v1 ? cv[v + u] : make_uint4(0, 0, 0, 0);
-      const uint32_t after = dilate ? at(16 * (v + 8 < v1 ? v + 8 : v1)) : 0u;
+      for (int u = 0; u < D; u++) q[u] = v + u < v1 ? cv[v + u] : make_uint4(0, 0, 0, 0);
+      const uint32_t after = dilate ? at(16 * (v + D < v1 ? v + D : v1)) : 0u;
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < D; u++) {
         if (v + u >= v1) break;
         const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
         if (!dilate) {
@@ -203,7 +241,7 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
           for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
           continue;
         }
-        const uint32_t nxt = u + 1 < 8 && v + u + 1 < v1 ? (q[u + 1].x & 0xffu) : after;
+        const uint32_t nxt = u + 1 < D && v + u + 1 < v1 ? (q[u + 1].x & 0xffu) : after;
         uint32_t cur = w[0] & 0xffu;
 #pragma unroll
         for (int e = 0; e < 16; e++) {
@@ -229,7 +267,9 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
   };
   // LDS atomics on the lane's own counters: no conflicts, and the count pass's
   // need no return (a plain read-modify-write would wait on every read)
-  pass([&](uint32_t b, int) { atomicAdd(&cnt[b][lane], 1u); });
+  auto count = [&](uint32_t b, int) { atomicAdd(&cnt[b][lane], 1u); };
+  if (dilate) pass(std::integral_constant<int, 4>{}, count);
+  else pass(std::integral_constant<int, 8>{}, count);
   uint32_t run = 0;  // exclusive scan over (bucket, lane), bucket-major
 #pragma unroll
   for (int b = 0; b < kTileBuckets; b++) {
@@ -243,7 +283,9 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
     cnt[b][lane] = run + incl - c;
     run += (uint32_t)__shfl((int)incl, 63, 64);
   }
-  pass([&](uint32_t b, int t) { order[atomicAdd(&cnt[b][lane], 1u)] = (uint32_t)t; });
+  auto place = [&](uint32_t b, int t) { order[atomicAdd(&cnt[b][lane], 1u)] = (uint32_t)t; };
+  if (dilate) pass(std::integral_constant<int, 4>{}, place);
+  else pass(std::integral_constant<int, 8>{}, place);
 }
 
 constexpr float kTinySqrtArg = 0x1.0p-96f;

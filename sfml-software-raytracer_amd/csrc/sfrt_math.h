@@ -149,6 +149,23 @@ SFRT_HD float div_recip(float a, float b, float y) {
   return __builtin_fmaf(r, y, q);
 }
 
+// (t - df*df) / (s + df) of e_asinf.c's |x| in [0.5, 0.975) branch.  There t is in
+// (0.0125, 0.25], so the numerator is +0 or a non-zero multiple of 2^-30 and the
+// denominator lies in (0.2, 1]: on the device the division runs as the compiler's
+// own correctly rounded sequence without its range scaling, which is the identity
+// for such operands (sfrt_device.h div_inrange has the argument); same bits as `/`.
+SFRT_HD float asinf_tail_div(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float y0 = __builtin_amdgcn_rcpf(b);
+  const float y = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
+  float q = a * y;
+  q = __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+  return __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+#else
+  return a / b;
+#endif
+}
+
 // e_asinf.c
 SFRT_HD float asinf(float x) {
   const float pio2_hi = u2f(0x3fc90fdbu);
@@ -176,7 +193,7 @@ SFRT_HD float asinf(float x) {
     r = pio2_hi - ((q + q) - pio2_lo);
   } else {
     const float df = u2f(f2u(s) & 0xfffff000u);
-    const float c = (t - df * df) / (s + df);
+    const float c = asinf_tail_div(t - df * df, s + df);
     const float pp = (s + s) * p - (pio2_lo - (c + c));
     const float q = pio4_hi - (df + df);
     r = pio4_hi - (pp - q);

@@ -48,9 +48,18 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
   float z = (f.fwd[2] + f.right[2] * h) + f.up[2] * v;
   // |(x,y,z)|^2 >= 1 - tiny: forward is a unit vector orthogonal to right and up
   const float len = sqrt_cr_normal((x * x + y * y) + z * z);
-  dx = x / len;
-  dy = y / len;
-  dz = z / len;
+  // components in [2^-40, 2^40) put len there too: one shared reciprocal seed
+  // (div_inrange, the same bits as `/`); a wave with a zero component takes `/`
+  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(x) & div_operand_ok(y) & div_operand_ok(z))) == 0) {
+    const float s = div_seed(len);
+    dx = div_inrange(x, len, s);
+    dy = div_inrange(y, len, s);
+    dz = div_inrange(z, len, s);
+  } else {
+    dx = x / len;
+    dy = y / len;
+    dz = z / len;
+  }
 }
 
 // Shading tail, SphereWorld.cpp:373-381.  Returns RGBA8 packed (r in byte 0).
@@ -60,11 +69,21 @@ __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d,
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
   const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
   const float ex = px - d.cx, ey = py - d.cy, ez = pz - d.cz;
-  const float ny = ey / sqrt_cr((ex * ex + ey * ey) + ez * ez);
-  const float ycoord = sfrt_math::div_pi_plus_half(sfrt_math::asinf(ny));  // == asinf / PI + 0.5f
+  const float el = sqrt_cr((ex * ex + ey * ey) + ez * ez);
   const float bx = px - f.cam[0], by = py - f.cam[1], bz = pz - f.cam[2];
   const float bl = sqrt_cr((bx * bx + by * by) + bz * bz);
-  const float brightness = 3.0f / (bl < 3.0f ? 3.0f : bl);
+  const float bd = bl < 3.0f ? 3.0f : bl;
+  // ey / el and 3 / bd through div_inrange (same bits) unless some lane's operands
+  // leave [2^-40, 2^40) (bd >= 3 needs only the upper bound)
+  float ny, brightness;
+  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(ey) & div_operand_ok(el) & (uint32_t)(bd < 0x1.0p40f))) == 0) {
+    ny = div_inrange(ey, el);
+    brightness = div_inrange(3.0f, bd);
+  } else {
+    ny = ey / el;
+    brightness = 3.0f / bd;
+  }
+  const float ycoord = sfrt_math::div_pi_plus_half(sfrt_math::asinf(ny));  // == asinf / PI + 0.5f
   // fmodf(v, 1.0f) == v - truncf(v) exactly for every binary32 v (NaN/inf -> NaN).
   // texsize of textures[0] (or of the sphere's extension slot), (float)(unsigned) as :376
   const uint32_t tw = d.tex_wh & 0xffffu, th = d.tex_wh >> 16;
@@ -237,7 +256,7 @@ __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int t
 // ss are (tests/native/wave_check.hip, every ss).
 template <int R>
 __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, float rad, int k,
-                                            float (&L)[R], int (&dnew)[R]) {
+                                            float (&L)[R], int (&draw)[R]) {
   uint64_t any = 0;
 #pragma unroll
   for (int r = 0; r < R; r++) any |= __builtin_amdgcn_ballot_w64(ss[r] < s_pass);
@@ -248,7 +267,7 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
       if (ss[r] < s_pass) {
         const float t = rad - sqrt_cr_normal(ss[r]);
         L[r] = max_nonneg(L[r], t);
-        dnew[r] = k;
+        draw[r] = k;
       }
     }
   }
@@ -272,7 +291,7 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
 //
 // A stopped ray advances unmasked: it had no passing sphere at its position
 // (its last step visited every sphere that could pass for it) and never moves
-// again, so each later step again has none: L = +0, dnew = draw, tacc + 0 =
+// again, so each later step again has none: L = +0, draw unchanged, tacc + 0 =
 // tacc, and p + d * (+0) = p -- also for p = -0, which a marching wave's ray
 // only reaches through -0 + d * l0 with d of negative sign, so d * (+0) = -0.
 // Edge lanes trace a clamped duplicate pixel (never stored) as the duplicate
@@ -377,33 +396,36 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   auto entry = [&](int e) { return LIST ? __builtin_amdgcn_readlane(cidx, e) : e; };
 
   // pos += dir * L (SphereWorld.cpp:371) on every lane (see above)
-  auto advance = [&](const float (&L)[R], const int (&dnew)[R]) {
+  auto advance = [&](const float (&L)[R]) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
       px[r] = px[r] + dx[r] * L[r];
       py[r] = py[r] + dy[r] * L[r];
       pz[r] = pz[r] + dz[r] * L[r];
-      draw[r] = dnew[r];
       mv[r] = L[r];
       tacc[r] = tacc[r] + L[r];
     }
   };
-  auto visit = [&](float cx, float cy, float cz, float rad, float s_pass, int k, float (&L)[R],
-                   int (&dnew)[R]) {
+  auto visit = [&](float cx, float cy, float cz, float rad, float s_pass, int k, float (&L)[R]) {
     float ss[R];
 #pragma unroll
     for (int r = 0; r < R; r++) ss[r] = dist2(px[r], py[r], pz[r], cx, cy, cz);
-    pass_body_r<R>(ss, s_pass, rad, k, L, dnew);
+    pass_body_r<R>(ss, s_pass, rad, k, L, draw);
   };
   // Every sphere in index order (no culling: cull off, or past kCullSafeIterations steps).
-  auto visit_all = [&](float (&L)[R], int (&dnew)[R]) {
+  auto visit_all = [&](float (&L)[R]) {
     for (int k = 0; k < f.n; k++) {
       const SphereRec& s = sph[k];
-      visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L, dnew);
+      visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L);
     }
   };
   int trips = 1;
-
+  // Culled steps run while trips < kCullSafeIterations (the margins' bound, sec. 4 of
+  // DESIGN.md); a wave still marching then continues in the full-list loop below.  Each
+  // loop is single-exit (the guard is its condition) with one body shape: a second exit,
+  // or a full/culled branch inside the step, makes the compiler copy every loop-carried
+  // register (draw, L) between register sets each step.
+  const int cull_end = full ? 1 : kCullSafeIterations;
 #ifdef SFRT_SLOTS
   constexpr int kSlotsR = SFRT_SLOTS;
 #else
@@ -428,76 +450,69 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         sk[q] = k;
       }
     }
-    // single-exit loop (the march guard is part of the condition): a second
-    // exit makes the compiler shuffle every loop-carried register each step
-    for (; any_marching() && trips < kMaxIterations; ++trips) {
-      if (trips == kCullSafeIterations) {  // uniform: leave culling behind, visit all
-#pragma unroll
-        for (int q = 0; q < kSlotsR; q++) ssp[q] = 0.0f;
-        full = true;
-      }
+    for (; any_marching() && trips < cull_end; ++trips) {
       float L[R];
-      int dnew[R];
 #pragma unroll
-      for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
+      for (int r = 0; r < R; r++) L[r] = 0.0f;
 #pragma unroll
-      for (int q = 0; q < kSlotsR; q++) visit(scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L, dnew);
-      if (full) visit_all(L, dnew);
-      advance(L, dnew);
+      for (int q = 0; q < kSlotsR; q++) visit(scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L);
+      advance(L);
     }
   } else {
     float tlo = 0.0f;
-    for (; any_marching() && trips < kMaxIterations; ++trips) {
-      if (trips == kCullSafeIterations) full = true;  // uniform: visit all from here on
+    for (; any_marching() && trips < cull_end; ++trips) {
       float L[R];
-      int dnew[R];
 #pragma unroll
-      for (int r = 0; r < R; r++) { L[r] = 0.0f; dnew[r] = draw[r]; }
-      if (full) {
-        visit_all(L, dnew);
-      } else {
-        // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32)
-        uint32_t th = 0u;  // +0
+      for (int r = 0; r < R; r++) L[r] = 0.0f;
+      // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32)
+      uint32_t th = 0u;  // +0
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint32_t u = __float_as_uint(tacc[r]);
+        th = u > th ? u : th;
+      }
+      if (trips % 2 == 1) {  // the low end, every second step
+        uint32_t tl = 0x7f800000u;  // +inf
 #pragma unroll
         for (int r = 0; r < R; r++) {
           const uint32_t u = __float_as_uint(tacc[r]);
-          th = u > th ? u : th;
+          const uint32_t ua = mv[r] > 0.0f ? u : 0x7f800000u;
+          tl = ua < tl ? ua : tl;
         }
-        if (trips % 2 == 1) {  // the low end, every second step
-          uint32_t tl = 0x7f800000u;  // +inf
-#pragma unroll
-          for (int r = 0; r < R; r++) {
-            const uint32_t u = __float_as_uint(tacc[r]);
-            const uint32_t ua = mv[r] > 0.0f ? u : 0x7f800000u;
-            tl = ua < tl ? ua : tl;
-          }
-          tlo = __uint_as_float(wave_min_u32(tl));
-        }
-        const float thi = __uint_as_float(wave_max_u32(th));
-        const uint64_t win =
-            m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
-        // The visits, in index order, each issuing the next record's scalar loads
-        // before its own arithmetic (the loads' latency hides under the R rays'
-        // distance tests; kn = k for the last visit reloads a record already in
-        // the scalar cache).
-        if (win) {
-          uint64_t mm = win;
-          int k = entry(__builtin_ctzll(mm));
+        tlo = __uint_as_float(wave_min_u32(tl));
+      }
+      const float thi = __uint_as_float(wave_max_u32(th));
+      const uint64_t win =
+          m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
+      // The visits, in index order, each issuing the next record's scalar loads
+      // before its own arithmetic (the loads' latency hides under the R rays'
+      // distance tests; kn = k for the last visit reloads a record already in
+      // the scalar cache).
+      if (win) {
+        uint64_t mm = win;
+        int k = entry(__builtin_ctzll(mm));
+        mm &= mm - 1;
+        float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
+        for (;;) {
+          const int kn = mm ? entry(__builtin_ctzll(mm)) : k;
+          const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
+                      nsp = sph[kn].s_pass;
+          visit(cx, cy, cz, rad, sp, k, L);
+          if (!mm) break;
           mm &= mm - 1;
-          float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
-          for (;;) {
-            const int kn = mm ? entry(__builtin_ctzll(mm)) : k;
-            const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
-                        nsp = sph[kn].s_pass;
-            visit(cx, cy, cz, rad, sp, k, L, dnew);
-            if (!mm) break;
-            mm &= mm - 1;
-            k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
-          }
+          k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
         }
       }
-      advance(L, dnew);
+      advance(L);
     }
+  }
+  // Every sphere in index order, every step: culling off, or past kCullSafeIterations.
+  for (; any_marching() && trips < kMaxIterations; ++trips) {
+    float L[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) L[r] = 0.0f;
+    visit_all(L);
+    advance(L);
   }
   if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
   if (f.tile_cost && lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket((uint32_t)trips);
@@ -526,7 +541,10 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 
 // n <= 64: the records travel in the kernel-argument segment.
 template <int R>
-__global__ __launch_bounds__(64) void k_trace_window_r(InlineArgs args) {
+#ifndef SFRT_R_WAVES
+#define SFRT_R_WAVES 8
+#endif
+__global__ __launch_bounds__(64, SFRT_R_WAVES) void k_trace_window_r(InlineArgs args) {
   trace_tile_window_r<R, false>(args.f, args.s);
 }
 

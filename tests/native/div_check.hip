@@ -1,11 +1,15 @@
 // gfx950 check of sfrt_math::div_recip(a, b, 1.0f / b) == a / b (correctly
-// rounded division), bit for bit, entirely on the device (no host compare).
+// rounded division, classes 0-2) and of sfrt::div_inrange(a, b) == a / b (the
+// compiler's division sequence without its range scaling, classes 3-4), bit for
+// bit, entirely on the device (no host compare).
 // Built and run by tests/test_gpu_parity.py::test_device_div_recip:
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off div_check.hip -o div_check
 //   ./div_check <log2 pairs per class>
 // Classes: random normal b in [2^-60, 2^60] with random a keeping a/b normal;
 // the voxel DDA domain (b in (2^-14, 1.5], a in [-0.25, 1.25]); b with
 // all-ones / one-ulp-off-a-power-of-two significands and dense a in [0, 2).
+// div_inrange: random a, b with |a|, |b| in [2^-40, 2^40) (every 64th a = +0 with
+// b > 0); b with hard significands in the same range and random a.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -14,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "../../sfml-software-raytracer_amd/csrc/sfrt_device.h"
 #include "../../sfml-software-raytracer_amd/csrc/sfrt_math.h"
 
 #pragma clang fp contract(off)
@@ -43,6 +48,20 @@ __global__ void k_check(int cls, unsigned long long iters, unsigned long long* b
       b = 1.5f * u01((uint32_t)z);
       if (b < 0x1.0p-14f) b = 0x1.0p-14f;
       a = -0.25f + 1.5f * u01((uint32_t)(z >> 32));
+    } else if (cls == 3 || cls == 4) {  // div_inrange operands: |a|, |b| in [2^-40, 2^40)
+      const uint32_t eb = 127 - 40 + (uint32_t)((z >> 40) % 80);
+      const uint32_t ea = 127 - 40 + (uint32_t)((z >> 48) % 80);
+      uint32_t mant = (uint32_t)z & 0x7fffffu;
+      if (cls == 4) {
+        const uint32_t kind = (uint32_t)(z >> 61);
+        mant = kind < 2 ? 0x7fffffu : (kind < 4 ? 0x000001u : (kind < 6 ? 0x7ffffeu : 0u));
+      }
+      b = sfrt_math::u2f((eb << 23) | mant | ((z >> 63) << 31));
+      a = sfrt_math::u2f((ea << 23) | ((uint32_t)(z >> 20) & 0x7fffffu) | (((z >> 62) & 1) << 31));
+      if (cls == 3 && ((z >> 8) & 63) == 0) {  // +0 over a positive b
+        a = 0.0f;
+        b = fabsf(b);
+      }
     } else {               // hard significands for b, dense a
       const uint32_t kind = (uint32_t)(z >> 61);
       const uint32_t eb = 127 - 20 + (uint32_t)((z >> 50) % 41);
@@ -51,7 +70,7 @@ __global__ void k_check(int cls, unsigned long long iters, unsigned long long* b
       a = sfrt_math::u2f((uint32_t)(127u << 23) | ((uint32_t)z & 0x7fffffu)) - 1.0f + u01((uint32_t)(z >> 32));
     }
     const float want = a / b;
-    const float got = sfrt_math::div_recip(a, b, 1.0f / b);
+    const float got = cls >= 3 ? sfrt::div_inrange(a, b) : sfrt_math::div_recip(a, b, 1.0f / b);
     const bool same = (want != want && got != got) || sfrt_math::f2u(want) == sfrt_math::f2u(got);
     if (!same) {
       nbad++;
@@ -69,7 +88,7 @@ int main(int argc, char** argv) {
   float* d_ex;
   if (hipMalloc(&d_bad, 8) || hipMalloc(&d_ex, 8)) return 3;
   unsigned long long total_bad = 0, total = 0;
-  for (int cls = 0; cls < 3; cls++) {
+  for (int cls = 0; cls < 5; cls++) {
     unsigned long long zero = 0;
     float ex[2] = {0, 0};
     hipMemcpy(d_bad, &zero, 8, hipMemcpyHostToDevice);
@@ -83,6 +102,6 @@ int main(int argc, char** argv) {
     total_bad += b;
     total += iters;
   }
-  printf("div_recip checked=%llu mismatches=%llu\n", total, total_bad);
+  printf("div_recip/div_inrange checked=%llu mismatches=%llu\n", total, total_bad);
   return total_bad ? 1 : 0;
 }

@@ -314,7 +314,8 @@ def test_device_math_matches_libm(fn, arg, tmp_path):
 
 
 def test_device_div_recip(tmp_path):
-    """sfrt_math::div_recip(a, b, 1/b) == a / b on gfx950 (3 x 2^33 pairs, DESIGN.md 4)."""
+    """sfrt_math::div_recip(a, b, 1/b) and sfrt::div_inrange(a, b) == a / b on gfx950
+    (5 classes x 2^33 pairs)."""
     exe = tmp_path / "div_check"
     src = os.path.join(ROOT, "tests", "native", "div_check.hip")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
