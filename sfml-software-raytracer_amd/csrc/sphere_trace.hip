@@ -62,9 +62,20 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
   }
 }
 
-// Shading tail, SphereWorld.cpp:373-381.  Returns RGBA8 packed (r in byte 0).
-__device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d, float px,
-                                         float py, float pz, PixelDump* dump) {
+// Shading tail, SphereWorld.cpp:373-381, in two parts so that a lane's R pixels
+// can issue their texel loads together: shade_texel computes the texel index --
+// `tex` indexes f.tex (the sphere's first texel when the index falls outside the
+// texture: the reference would read outside the image there; `outside` reports
+// it) -- and the brightness; shade_rgba applies the brightness (RGBA8 packed, r
+// in byte 0).
+struct Shading {
+  uint32_t tex;
+  float brightness;
+  bool outside;
+};
+
+__device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRec& d, float px,
+                                               float py, float pz, PixelDump* dump) {
   float ang = d.atan_c - atan2f_wave(pz, px);  // == sfrt_math::atan2f (sfrt_device.h)
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
   const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
@@ -94,24 +105,35 @@ __device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d,
   // float -> unsigned: v_cvt_u32_f32 (NaN -> 0), as x86's cvttss2si for [0, 2^31).
   const uint32_t tx = __float2uint_rz(u), ty = __float2uint_rz(w);
   const uint32_t idx = tx + ty * tw;
-  uint32_t texel = 0;
-  if (idx < tw * th) {
-    texel = f.tex[d.tex_off + idx];
-  } else {
-    atomicOr(f.status, 2);  // the reference would read outside the image here
-  }
-  const uint32_t r = __float2uint_rz((float)(texel & 0xffu) * brightness);
-  const uint32_t g = __float2uint_rz((float)((texel >> 8) & 0xffu) * brightness);
-  const uint32_t b = __float2uint_rz((float)((texel >> 16) & 0xffu) * brightness);
-  const uint32_t rgba = (r & 0xffu) | ((g & 0xffu) << 8) | ((b & 0xffu) << 16) | (texel & 0xff000000u);
+  Shading sh;
+  sh.outside = !(idx < tw * th);
+  sh.tex = d.tex_off + (sh.outside ? 0u : idx);
+  sh.brightness = brightness;
   if (dump) {
     dump->xcoord = xcoord;
     dump->ycoord = ycoord;
     dump->brightness = brightness;
     dump->texel[0] = tx;
     dump->texel[1] = ty;
-    dump->rgba = rgba;
   }
+  return sh;
+}
+
+// (Uint8)(component * brightness) for r, g, b; alpha kept (:377-379, :109).
+__device__ __forceinline__ uint32_t shade_rgba(uint32_t texel, float brightness) {
+  const uint32_t r = __float2uint_rz((float)(texel & 0xffu) * brightness);
+  const uint32_t g = __float2uint_rz((float)((texel >> 8) & 0xffu) * brightness);
+  const uint32_t b = __float2uint_rz((float)((texel >> 16) & 0xffu) * brightness);
+  return (r & 0xffu) | ((g & 0xffu) << 8) | ((b & 0xffu) << 16) | (texel & 0xff000000u);
+}
+
+// Both parts for one pixel (the parity kernel k_trace_points).
+__device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d, float px,
+                                         float py, float pz, PixelDump* dump) {
+  const Shading sh = shade_texel(f, d, px, py, pz, dump);
+  if (sh.outside) atomicOr(f.status, 2);
+  const uint32_t rgba = shade_rgba(sh.outside ? 0u : f.tex[sh.tex], sh.brightness);
+  if (dump) dump->rgba = rgba;
   return rgba;
 }
 
@@ -246,6 +268,21 @@ __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int t
   return c;
 }
 
+
+// L = +0 for a lane's R rays at the start of a march step, two registers per
+// v_mov_b64 (left to itself the compiler copies one zero register into three
+// others and then pairs them: five moves a step for R = 4, not two).
+template <int R>
+__device__ __forceinline__ void zero_steps(float (&L)[R]) {
+#pragma unroll
+  for (int r = 0; r + 1 < R; r += 2) {
+    uint64_t z;
+    __asm__ volatile("v_mov_b64 %0, 0" : "=v"(z));
+    L[r] = __uint_as_float((uint32_t)z);
+    L[r + 1] = __uint_as_float((uint32_t)(z >> 32));
+  }
+  if (R & 1) L[R - 1] = 0.0f;
+}
 
 // Pass bodies of one sphere for the lane's R rays under one scalar branch.
 // (Lane-masked selects through inline asm instead of these exec-masked
@@ -452,8 +489,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
     for (; any_marching() && trips < cull_end; ++trips) {
       float L[R];
-#pragma unroll
-      for (int r = 0; r < R; r++) L[r] = 0.0f;
+      zero_steps<R>(L);
 #pragma unroll
       for (int q = 0; q < kSlotsR; q++) visit(scx[q], scy[q], scz[q], sr[q], ssp[q], sk[q], L);
       advance(L);
@@ -462,8 +498,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     float tlo = 0.0f;
     for (; any_marching() && trips < cull_end; ++trips) {
       float L[R];
-#pragma unroll
-      for (int r = 0; r < R; r++) L[r] = 0.0f;
+      zero_steps<R>(L);
       // tacc >= +0: reduce the bit patterns (wave_min_u32 / wave_max_u32)
       uint32_t th = 0u;  // +0
 #pragma unroll
@@ -509,26 +544,40 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   // Every sphere in index order, every step: culling off, or past kCullSafeIterations.
   for (; any_marching() && trips < kMaxIterations; ++trips) {
     float L[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) L[r] = 0.0f;
+    zero_steps<R>(L);
     visit_all(L);
     advance(L);
   }
   if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
   if (f.tile_cost && lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket((uint32_t)trips);
+#if SFRT_EXP & 64  // timing probe only (wrong bytes): the march without the shading tail
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (valid[r])
+      f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] =
+          __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^ __float_as_uint(pz[r]) ^ (uint32_t)draw[r];
+#else
+  // Shading: the R records gathered first, then the R texel indices, the R texel
+  // loads back to back, and the stores.  Edge lanes shade their duplicates too
+  // (same values as the real pixel) and store nothing.
+  SphereRec d[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) d[r] = sph[draw[r]];
+  Shading sh[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) sh[r] = shade_texel(f, d[r], px[r], py[r], pz[r], nullptr);
+  uint32_t texel[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) texel[r] = f.tex[sh[r].tex];
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (valid[r]) {
-#if SFRT_EXP & 64  // timing probe only (wrong bytes): the march without the shading tail
+      if (sh[r].outside) atomicOr(f.status, 2);  // the reference would read outside the image
       f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] =
-          __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^ __float_as_uint(pz[r]) ^ (uint32_t)draw[r];
-      continue;
-#endif
-      const SphereRec d = sph[draw[r]];
-      const uint32_t rgba = shade(f, d, px[r], py[r], pz[r], nullptr);
-      f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] = rgba;
+          shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
     }
   }
+#endif
 #if SFRT_EXP & 16
   const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
   if (lane < 4 && valid[0]) {
