@@ -89,9 +89,10 @@ __device__ __forceinline__ float div_inrange(float a, float b, float y) {
 __device__ __forceinline__ float div_inrange(float a, float b) { return div_inrange(a, b, div_seed(b)); }
 
 // |v| in [2^-40, 2^40) (so finite, non-zero, normal): two quotients of such
-// values are normal and every precondition of div_inrange holds.
-__device__ __forceinline__ uint32_t div_operand_ok(float v) {  // 0 / 1, combined with &
-  return (sfrt_math::f2u(v) & 0x7fffffffu) - 0x2b800000u < 0x53800000u - 0x2b800000u;
+// values are normal and every precondition of div_inrange holds.  Two compares
+// with |v| as a source modifier (NaN fails both), combined in the SGPR masks.
+__device__ __forceinline__ bool div_operand_ok(float v) {
+  return __builtin_fabsf(v) >= 0x1.0p-40f && __builtin_fabsf(v) < 0x1.0p40f;
 }
 
 // atan2f(y, x), bit for bit sfrt_math::atan2f (= glibc's e_atan2f.c), with a
@@ -112,8 +113,8 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
   // all rare, takes the general code, like one with |y/x| outside [2^-29, 2^25))
   const float q = div_inrange(y, x);
   const uint32_t iq = f2u(q) & 0x7fffffffu;
-  const bool general = div_operand_ok(x) & div_operand_ok(y) &
-                       (uint32_t)(iq - 0x31000000u < 0x4c000000u - 0x31000000u);
+  const bool general = div_operand_ok(x) && div_operand_ok(y) &&
+                       (iq - 0x31000000u < 0x4c000000u - 0x31000000u);
   if (__builtin_amdgcn_ballot_w64(!general)) return sfrt_math::atan2f(y, x);
   const float a = u2f(iq);
   const int id = iq < 0x3ee00000u ? -1

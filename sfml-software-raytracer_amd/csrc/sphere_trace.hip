@@ -50,7 +50,7 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
   const float len = sqrt_cr_normal((x * x + y * y) + z * z);
   // components in [2^-40, 2^40) put len there too: one shared reciprocal seed
   // (div_inrange, the same bits as `/`); a wave with a zero component takes `/`
-  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(x) & div_operand_ok(y) & div_operand_ok(z))) == 0) {
+  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(x) && div_operand_ok(y) && div_operand_ok(z))) == 0) {
     const float s = div_seed(len);
     dx = div_inrange(x, len, s);
     dy = div_inrange(y, len, s);
@@ -87,7 +87,7 @@ __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRe
   // ey / el and 3 / bd through div_inrange (same bits) unless some lane's operands
   // leave [2^-40, 2^40) (bd >= 3 needs only the upper bound)
   float ny, brightness;
-  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(ey) & div_operand_ok(el) & (uint32_t)(bd < 0x1.0p40f))) == 0) {
+  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(ey) && div_operand_ok(el) && bd < 0x1.0p40f)) == 0) {
     ny = div_inrange(ey, el);
     brightness = div_inrange(3.0f, bd);
   } else {
@@ -363,17 +363,15 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   const int bc = b < b_end ? b : b_end - 1;
   const int j = f.ystart + bc * f.yadd;
   const float l0 = f.first_l;
-  int a[R], draw[R];
-  bool valid[R];
+  int draw[R];
   float dx[R], dy[R], dz[R], px[R], py[R], pz[R], mv[R], tacc[R];
   // mv: the ray's last step length (> 0 while it marches, +0 once it stopped);
   // `mv > 0` is one compare per step, where a loop-carried bool would be
   // rematerialised through VGPRs.
 #pragma unroll
   for (int r = 0; r < R; r++) {
-    a[r] = tile_x * R * kTile + r * kTile + (lane & 7);
-    valid[r] = a[r] < f.sub_w && b < b_end;
-    const int ac = a[r] < f.sub_w ? a[r] : f.sub_w - 1;
+    const int a = tile_x * R * kTile + r * kTile + (lane & 7);
+    const int ac = a < f.sub_w ? a : f.sub_w - 1;
     primary_dir(f, f.xstart + ac * f.xadd, j, dx[r], dy[r], dz[r]);
     px[r] = f.cam[0] + dx[r] * l0;
     py[r] = f.cam[1] + dy[r] * l0;
@@ -550,11 +548,19 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   }
   if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
   if (f.tile_cost && lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket((uint32_t)trips);
+  // Pixel (a, b) of ray r, recomputed here from a fresh lane id (mbcnt, so that the
+  // compiler does not reuse the kernel entry's values): kept from there, the columns sat
+  // in registers through the whole march, and at R = 4 one of them was spilled.
+  const int lane_s = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int b_s = f.sub_row0 + tile_y * kTile + (lane_s >> 3);
+  auto col = [&](int r) { return tile_x * R * kTile + r * kTile + (lane_s & 7); };
+  auto valid = [&](int r) { return col(r) < f.sub_w && b_s < b_end; };
+  auto px_out = [&](int r) { return f.out + (long long)(b_s - f.sub_row0) * f.out_pitch + col(r); };
 #if SFRT_EXP & 64  // timing probe only (wrong bytes): the march without the shading tail
 #pragma unroll
   for (int r = 0; r < R; r++)
-    if (valid[r])
-      f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] =
+    if (valid(r))
+      *px_out(r) =
           __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^ __float_as_uint(pz[r]) ^ (uint32_t)draw[r];
 #else
   // Shading: the R records gathered first, then the R texel indices, the R texel
@@ -571,19 +577,18 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   for (int r = 0; r < R; r++) texel[r] = f.tex[sh[r].tex];
 #pragma unroll
   for (int r = 0; r < R; r++) {
-    if (valid[r]) {
+    if (valid(r)) {
       if (sh[r].outside) atomicOr(f.status, 2);  // the reference would read outside the image
-      f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[r]] =
-          shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
+      *px_out(r) = shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
     }
   }
 #endif
 #if SFRT_EXP & 16
   const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
-  if (lane < 4 && valid[0]) {
+  if (lane < 4 && valid(0)) {
     const uint32_t v = lane == 0 ? (uint32_t)dbg_t0 : lane == 1 ? (uint32_t)dbg_t1
                      : lane == 2 ? (uint32_t)trips : (uint32_t)slot;
-    f.out[(long long)(b - f.sub_row0) * f.out_pitch + a[0]] = v;
+    *px_out(0) = v;
   }
 #endif
 }
@@ -599,7 +604,10 @@ __global__ __launch_bounds__(64, SFRT_R_WAVES) void k_trace_window_r(InlineArgs 
 
 // n > 64: the records in device memory (f.spheres), the culled list per wave.
 template <int R>
-__global__ __launch_bounds__(64) void k_trace_window_list(FrameRec f) {
+#ifndef SFRT_LIST_WAVES
+#define SFRT_LIST_WAVES 1
+#endif
+__global__ __launch_bounds__(64, SFRT_LIST_WAVES) void k_trace_window_list(FrameRec f) {
   trace_tile_window_r<R, true>(f, f.spheres);
 }
 

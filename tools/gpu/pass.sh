@@ -1,6 +1,6 @@
 # One GPU pass: the whole -m gpu suite, smoke(), the default bench line, then a kernel
 # trace of the same bench command (the profile the bench line's kernel time must agree with).
-#   TAG=r2a /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu/pass.sh
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- "TAG=r2a bash tools/gpu/pass.sh"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

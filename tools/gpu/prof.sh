@@ -1,5 +1,5 @@
 # Kernel trace + PMC passes of the default bench command (profiles/<tag>_*):
-#   TAG=r2c /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/gpu/prof.sh
+#   /usr/local/graft/bin/gpurun --timeout 900 -- "TAG=r2c bash tools/gpu/prof.sh"
 # then: python tools/rocprof_summary.py --trace gpurun_out/$TAG/trace --fetch gpurun_out/$TAG/pmc_fetch
 #       --write gpurun_out/$TAG/pmc_write --sq gpurun_out/$TAG/pmc_sq gpurun_out/$TAG/pmc_sq2 --tag $TAG
 set -o pipefail
