@@ -151,17 +151,36 @@ def settle(world, pitch, row0, rows, stream, seconds: float) -> None:
     del buf
 
 
+def frame_row_costs(world, rank, world_size, height, pitch, stream):
+    """The frame's per-row work (sfrt_world_row_costs) on every rank: each rank renders its
+    equal band once in the adaptive tile order, and the bands' costs are summed over ranks
+    into one full-height vector (SURVEY 8e "Balance": cost-weighted band edges)."""
+    r0, n = band_of(rank, world_size, height)
+    buf = torch.empty(max(n, 1), pitch, dtype=torch.uint8, device="cuda")
+    world.render_band(buf.data_ptr(), pitch, r0, n, stream.cuda_stream)
+    c0, cost = world.row_costs()
+    full = torch.zeros(height, dtype=torch.float64, device="cuda")
+    full[c0:c0 + cost.size] = torch.from_numpy(cost.astype(np.float64)).to("cuda")
+    dist.all_reduce(full)
+    del buf
+    return full.cpu().numpy().astype(np.float32)
+
+
 def tuned_pipeline(world, rank, world_size, height, pitch, stream):
-    """Row bands for this node: tune_spans times a few root-weighted partitions with
-    real frames (untimed warm-up) and keeps the fastest; N = 1 is one whole band."""
+    """Row bands for this node: tune_spans times root-weighted and cost-weighted partitions
+    with real frames (untimed warm-up) and keeps the fastest; N = 1 is one whole band."""
     def render(band, row0, rows):
         world.render_band(band.data_ptr(), pitch, row0, rows, stream.cuda_stream)
-    spans, factor, table = tune_spans(render, rank, world_size, height, pitch, "cuda",
-                                      sync=torch.cuda.synchronize, reduce_device="cuda")
+    row_cost = frame_row_costs(world, rank, world_size, height, pitch, stream) \
+        if world_size > 1 else None
+    spans, pick, table = tune_spans(render, rank, world_size, height, pitch, "cuda",
+                                    sync=torch.cuda.synchronize, reduce_device="cuda",
+                                    row_cost=row_cost)
     pipe = BandPipeline(rank, world_size, height, pitch, "cuda", spans=spans)
-    info = {"rows_per_rank": [n for _, n in spans], "root_factor": factor}
+    info = {"rows_per_rank": [n for _, n in spans], "root_factor": pick["root_factor"],
+            "weights": pick["weights"]}
     if table:
-        info["tuning_ms_per_frame"] = {str(k): v for k, v in table.items()}
+        info["tuning_ms_per_frame"] = table
     return pipe, info
 
 

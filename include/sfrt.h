@@ -118,6 +118,14 @@ SFRT_API int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart,
 SFRT_API int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes, int row0,
                            int rows, void* hip_stream);
 SFRT_API int sfrt_world_check(sfrt_world* w, void* hip_stream);
+/* Estimated work per pixel row of the world's last frame fill that ran in the adaptive
+ * tile order (sfrt_world_render_band, sfrt_world_submit_frame; SFRT_OPT_TILE_ORDER on):
+ * *row0, *rows = the global rows it covered, costs[i] (i < *rows <= capacity) = the
+ * ray-steps of row *row0 + i, from the per-tile march-step classes that launch recorded
+ * (each pixel costs its tile's class steps plus ~4 for shading).  For cost-weighted row
+ * bands (sfrt_multi_cost_bands).  Synchronises with that fill; SFRT_E_INVALID if no
+ * such fill exists (or capacity is short). */
+SFRT_API int sfrt_world_row_costs(sfrt_world* w, float* costs, int capacity, int* row0, int* rows);
 
 /* Pipelined frame fill for the display path: renders the
  * whole width x height frame of the world's current state into `pixels`
@@ -205,6 +213,19 @@ SFRT_API int sfrt_multi_set_bands(sfrt_multi* m, const int* rows, int n);
  * multiples of the 8-row tile); root_factor 1 = equal split
  * [r*H/n, (r+1)*H/n). */
 SFRT_API int sfrt_multi_bands(int height, int n, float root_factor, int* row0, int* rows);
+/* Cost-weighted partition (SURVEY 8e "Balance"; stateless, no device): rank 0 gets
+ * `root_factor` shares of the frame's march cost sum(row_cost[0..height)), every
+ * other rank one share; band edges on 8-row tile boundaries (or the last row).
+ * row_cost: per-row work, e.g. from sfrt_world_row_costs / sfrt_multi_row_costs.
+ * Invalid or all-zero costs give sfrt_multi_bands' partition. */
+SFRT_API int sfrt_multi_cost_bands(const float* row_cost, int height, int n, float root_factor,
+                                   int* row0, int* rows);
+/* Per-row march cost of the whole frame from every rank's last band render
+ * (sfrt_world_row_costs of each rank's world; costs[height]).  Synchronises. */
+SFRT_API int sfrt_multi_row_costs(sfrt_multi* m, float* costs, int height);
+/* Re-partition from the last frame's row costs: sfrt_multi_row_costs +
+ * sfrt_multi_cost_bands + sfrt_multi_set_bands.  Call after a frame was rendered. */
+SFRT_API int sfrt_multi_balance(sfrt_multi* m, float root_factor);
 /* Render the whole width x height frame into `dev_frame` (device memory on
  * devices[0], pitch exactly width*4), asynchronously: every rank starts after
  * the work already queued on `hip_stream` (a stream of devices[0]; NULL = null

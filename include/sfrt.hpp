@@ -225,6 +225,9 @@ class MultiSphereWorld {
     check(sfrt_multi_set_bands(m_, rows.empty() ? nullptr : rows.data(), (int)rows.size()),
           "set_bands");
   }
+  // Cost-weighted bands from the last frame's per-row march work (sfrt_multi_balance):
+  // rank 0 (no link) gets root_factor shares of the work, every other GPU one share.
+  void Balance(float root_factor = 1.0f) { check(sfrt_multi_balance(m_, root_factor), "balance"); }
   // The whole frame into a caller-owned sf::Uint8* RGBA8 buffer (width*height*4).
   void UpdateImage(uint8_t* pixels) {
     push_state();

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -59,6 +60,45 @@ def root_weighted_spans(height: int, world: int, factor: float,
         return equal_spans(height, world)
     first = height - (world - 1) * other
     return [(0, first)] + [(first + (r - 1) * other, other) for r in range(1, world)]
+
+
+def cost_weighted_spans(row_cost, world: int, factor: float = 1.0,
+                        align: int = ALIGN) -> list[tuple[int, int]]:
+    """(row0, rows) per rank from per-row work (SURVEY 8e "Balance": cost-weighted band
+    edges): rank 0 gets `factor` shares of the frame's total cost, every other rank one
+    share.  Edges sit on `align`-row boundaries (or the last row); each is the boundary
+    whose cost prefix is closest to its target, never before the previous edge.  The
+    C ABI's sfrt_multi_cost_bands computes the same partition (same double sums in row
+    order, same ties).  Costs that are negative, non-finite or all zero fall back to
+    root_weighted_spans."""
+    height = len(row_cost)
+    at, pre = [], []
+    total, ok = 0.0, True
+    for j in range(height + 1):
+        if j % align == 0 or j == height:
+            at.append(j)
+            pre.append(total)
+        if j < height:
+            c = float(row_cost[j])
+            if not (c >= 0.0) or c == float("inf"):
+                ok = False
+            total += c
+    if world == 1 or not ok or not total > 0.0:
+        return root_weighted_spans(height, world, factor, align)
+    factor = float(np.float32(factor))  # the C ABI takes a binary32 factor
+    denom = (world - 1) + factor
+    edges, i = [0], 0
+    for r in range(1, world):
+        target = total * (factor + (r - 1)) / denom
+        k = i
+        while k + 1 < len(at) and pre[k] < target:
+            k += 1
+        if k > i and pre[k] - target > target - pre[k - 1]:
+            k -= 1
+        i = k
+        edges.append(at[i])
+    edges.append(height)
+    return [(edges[r], edges[r + 1] - edges[r]) for r in range(world)]
 
 
 def check_spans(spans, height: int) -> None:
@@ -176,19 +216,26 @@ def run_frames(pipe: BandPipeline, render, frames: int, sync=lambda: None) -> fl
 
 def tune_spans(render, rank: int, world_size: int, height: int, pitch: int, device,
                factors=DEFAULT_FACTORS, frames: int = 8, warm: int = 2,
-               sync=lambda: None, reduce_device="cpu"):
-    """Pick the root factor whose pipelined frames run fastest on this node.
+               sync=lambda: None, reduce_device="cpu", row_cost=None):
+    """Pick the partition whose pipelined frames run fastest on this node.
 
-    Every candidate partition runs `warm` + `frames` real frames through a
-    BandPipeline; the time that counts is the max over ranks (all-reduced, so
-    every rank sees the same numbers and takes the same decision).  Returns
-    (spans, factor, {factor: ms per frame})."""
+    Candidates: root_weighted_spans for every factor and, given the frame's per-row work
+    `row_cost` (sfrt_world_row_costs, the same on every rank), cost_weighted_spans for
+    every factor.  Every candidate runs `warm` + `frames` real frames through a
+    BandPipeline; the time that counts is the max over ranks (all-reduced, so every
+    rank sees the same numbers and takes the same decision).  Returns (spans, pick,
+    {label: ms per frame}) with pick = {"root_factor": f, "weights": "rows" | "cost"}
+    and labels "f" / "cost:f"."""
     if world_size == 1:
-        return [(0, height)], 1.0, {}
+        return [(0, height)], {"root_factor": 1.0, "weights": "rows"}, {}
+    cands = [(f"{f}", {"root_factor": f, "weights": "rows"}, root_weighted_spans(height, world_size, f))
+             for f in factors]
+    if row_cost is not None:
+        cands += [(f"cost:{f}", {"root_factor": f, "weights": "cost"},
+                   cost_weighted_spans(row_cost, world_size, f)) for f in factors]
     table, best = {}, None
     tried = set()
-    for f in factors:
-        spans = root_weighted_spans(height, world_size, f)
+    for label, pick, spans in cands:
         key = tuple(spans)
         if key in tried:
             continue
@@ -198,7 +245,7 @@ def tune_spans(render, rank: int, world_size: int, height: int, pitch: int, devi
         wall = max_over_ranks(run_frames(pipe, render, frames, sync), reduce_device)
         del pipe
         ms = wall / frames * 1e3
-        table[f] = round(ms, 4)
+        table[label] = round(ms, 4)
         if best is None or ms < best[0]:
-            best = (ms, f, spans)
+            best = (ms, pick, spans)
     return best[2], best[1], table

@@ -86,6 +86,44 @@ void split_rows(int height, int n, double factor, int* row0, int* rows) {
   }
 }
 
+// bands.py cost_weighted_spans, restated (row for row the same partition): rank 0 gets
+// `factor` shares of the frame's march cost, every other rank one share (SURVEY 8e
+// "Balance": cost-weighted band edges), with band edges on 8-row tile boundaries (or
+// the last row).  Each edge is the boundary whose cost prefix (a double sum over the rows
+// in order) is closest to its target, never before the previous edge.  Costs that are
+// negative, non-finite or sum to zero give split_rows' partition.
+void cost_rows(const float* cost, int height, int n, double factor, int* row0, int* rows) {
+  std::vector<int> at;  // candidate edges 0, 8, 16, ..., height
+  std::vector<double> pre;
+  double sum = 0.0;
+  bool ok = true;
+  for (int j = 0; j <= height; j++) {
+    if (j % kAlign == 0 || j == height) {
+      at.push_back(j);
+      pre.push_back(sum);
+    }
+    if (j < height) {
+      const double c = (double)cost[j];
+      if (!(c >= 0.0) || !std::isfinite(c)) ok = false;
+      sum += c;
+    }
+  }
+  if (n == 1 || !ok || !(sum > 0.0)) return split_rows(height, n, factor, row0, rows);
+  const double denom = (double)(n - 1) + factor;
+  size_t i = 0;
+  row0[0] = 0;
+  for (int r = 1; r < n; r++) {
+    const double target = sum * (factor + (double)(r - 1)) / denom;
+    size_t k = i;
+    while (k + 1 < at.size() && pre[k] < target) k++;
+    if (k > i && pre[k] - target > target - pre[k - 1]) k--;
+    i = k;
+    row0[r] = at[i];
+    rows[r - 1] = row0[r] - row0[r - 1];
+  }
+  rows[n - 1] = height - row0[n - 1];
+}
+
 struct Rank {
   int device = 0;
   sfrt_world* world = nullptr;
@@ -418,6 +456,49 @@ int sfrt_multi_bands(int height, int n, float root_factor, int* row0, int* rows)
     return SFRT_E_INVALID;
   split_rows(height, n, (double)root_factor, row0, rows);
   return SFRT_OK;
+}
+
+int sfrt_multi_cost_bands(const float* row_cost, int height, int n, float root_factor, int* row0,
+                          int* rows) {
+  if (height < 0 || n <= 0 || !row0 || !rows || (height > 0 && !row_cost) ||
+      !std::isfinite(root_factor) || root_factor <= 0.0f)
+    return SFRT_E_INVALID;
+  cost_rows(row_cost, height, n, (double)root_factor, row0, rows);
+  return SFRT_OK;
+}
+
+int sfrt_multi_row_costs(sfrt_multi* m, float* costs, int height) {
+  if (!m || height < 0 || (height > 0 && !costs)) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(m->mu);
+  std::vector<char> seen((size_t)height, 0);
+  for (auto& R : m->ranks) {
+    int r0 = 0, nr = 0, w = 0, h = 0;
+    int rc = sfrt_world_get_size(R.world, &w, &h);
+    if (rc) return rc;
+    if (h != height) return SFRT_E_INVALID;
+    std::vector<float> c((size_t)height);
+    if ((rc = sfrt_world_row_costs(R.world, c.data(), height, &r0, &nr))) return rc;
+    for (int j = 0; j < nr; j++) {
+      costs[r0 + j] = c[(size_t)j];
+      seen[(size_t)(r0 + j)] = 1;
+    }
+  }
+  for (char v : seen)
+    if (!v) return SFRT_E_INVALID;  // some row was not in any rank's last band
+  return SFRT_OK;
+}
+
+int sfrt_multi_balance(sfrt_multi* m, float root_factor) {
+  if (!m || !std::isfinite(root_factor) || root_factor <= 0.0f) return SFRT_E_INVALID;
+  int width = 0, height = 0;
+  int rc = sfrt_world_get_size(m->ranks[0].world, &width, &height);
+  if (rc) return rc;
+  std::vector<float> cost((size_t)height);
+  if ((rc = sfrt_multi_row_costs(m, cost.data(), height))) return rc;
+  const int n = (int)m->ranks.size();
+  std::vector<int> row0((size_t)n), rows((size_t)n);
+  cost_rows(cost.data(), height, n, (double)root_factor, row0.data(), rows.data());
+  return sfrt_multi_set_bands(m, rows.data(), n);
 }
 
 int sfrt_multi_render(sfrt_multi* m, void* dev_frame, int64_t pitch_bytes, void* hip_stream) {

@@ -13,6 +13,7 @@
 // evaluated exactly as the reference writes it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -328,7 +329,9 @@ struct sfrt_world {
     long long tiles = 0;
     const long long key = tile_order_on ? sfrt::trace_tile_key(f, &tiles) : 0;
     sfrt::TileSchedPtrs p;
+    const long long cap0 = sched.cap;
     HIP_TRY(sched.begin(key, tiles, s, tile_order_on, p));
+    if (sched.cap != cap0) last_fill.valid = false;  // the cost buffers were reallocated
     f.tile_order = p.tile_order;
     f.tile_cost = p.tile_cost;
     f.prev_cost = p.prev_cost;
@@ -346,11 +349,26 @@ struct sfrt_world {
     HIP_TRY(sched.end(p, s, queued));
     if (!queued) {
       chain_last.valid = false;
+      last_fill.valid = false;
       return SFRT_E_HIP;
     }
-    if (sched.committed) chain_last = ChainCam{true, cam, f.sub_row0};
+    if (sched.committed) {
+      chain_last = ChainCam{true, cam, f.sub_row0};
+      // that launch wrote its classes into cost[k % 2] before end() advanced k
+      last_fill = LastFill{true, f.sub_row0, f.sub_rows, f.sub_w, sched.key_prev,
+                           (int)((sched.k - 1) & 1)};
+    }
     return SFRT_OK;
   }
+
+  // The last launch that recorded its per-tile march-step classes (sfrt_world_row_costs).
+  struct LastFill {
+    bool valid = false;
+    int row0 = 0, rows = 0, width = 0;
+    long long key = 0;  // trace_tile_key: pixels per lane and the tile grid
+    int buf = 0;        // sched.cost[buf]
+  };
+  LastFill last_fill;
 
   // The camera of the last launch that joined the tile-order chain: its costs are the
   // ones the next launch's sorter ranks.
@@ -372,7 +390,57 @@ struct sfrt_world {
   }
 };
 
+namespace {
+
+// Representative march steps of a tile-order class (the inverse of sfrt_device.h
+// tile_bucket: class 15 - c holds steps < 4 for c = 0, 2c + 2 .. 2c + 3 for c = 1..6,
+// 16 + 4 (c - 7) .. + 3 for c = 7..10, then 32-39, 40-47, 48-63, 64-95, >= 96).
+double class_steps(uint8_t cls) {
+  const int c = 15 - (int)(cls & 15);
+  if (c == 0) return 3.0;
+  if (c <= 6) return 2.0 * c + 2.5;
+  if (c <= 10) return 16.0 + 4.0 * (c - 7) + 1.5;
+  static const double tail[5] = {35.5, 43.5, 55.5, 79.5, 128.0};
+  return tail[c - 11];
+}
+
+// The shading tail costs about as much as four march steps per pixel (22% of
+// the 4K frame, whose tiles march ~14 steps).
+constexpr double kShadeSteps = 4.0;
+
+}  // namespace
+
 extern "C" {
+
+int sfrt_world_row_costs(sfrt_world* w, float* costs, int capacity, int* row0, int* rows) {
+  if (!w || !row0 || !rows || capacity < 0 || (capacity > 0 && !costs)) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  *row0 = 0;
+  *rows = 0;
+  const auto& L = w->last_fill;
+  if (!L.valid) return SFRT_E_INVALID;
+  const int tile_w = (int)((L.key >> 56) & 0x3f) * sfrt::kTile;
+  const long long tiles_x = (L.key >> 28) & 0xfffffff, tiles_y = L.key & 0xfffffff;
+  if (tile_w <= 0 || tiles_x * tiles_y > w->sched.cap) return SFRT_E_INVALID;
+  if (capacity < L.rows) return SFRT_E_INVALID;
+  sfrt::DeviceGuard g(w->device);
+  if (w->sched.have_last) HIP_TRY(hipStreamSynchronize(w->sched.last_stream));
+  std::vector<uint8_t> cls((size_t)(tiles_x * tiles_y));
+  HIP_TRY(hipMemcpy(cls.data(), w->sched.cost[L.buf], cls.size(), hipMemcpyDeviceToHost));
+  for (long long ty = 0; ty < tiles_y; ty++) {
+    double c = 0.0;
+    for (long long tx = 0; tx < tiles_x; tx++) {
+      const long long x0 = tx * tile_w;
+      const long long px = std::min<long long>(tile_w, L.width - x0);
+      c += (class_steps(cls[(size_t)(ty * tiles_x + tx)]) + kShadeSteps) * (double)px;
+    }
+    for (int j = (int)ty * sfrt::kTile; j < std::min(L.rows, (int)(ty + 1) * sfrt::kTile); j++)
+      costs[j] = (float)c;
+  }
+  *row0 = L.row0;
+  *rows = L.rows;
+  return SFRT_OK;
+}
 
 int sfrt_world_create(int hip_device, sfrt_world** out) {
   if (!out) return SFRT_E_INVALID;

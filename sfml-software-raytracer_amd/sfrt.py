@@ -52,6 +52,7 @@ ABI_SYMBOLS = (
     "sfrt_multi_set_spheres", "sfrt_multi_add_sphere", "sfrt_multi_update_spheres",
     "sfrt_multi_set_sphere_textures", "sfrt_multi_set_option", "sfrt_multi_set_bands",
     "sfrt_multi_bands", "sfrt_multi_render", "sfrt_multi_check", "sfrt_multi_update_image",
+    "sfrt_world_row_costs", "sfrt_multi_cost_bands", "sfrt_multi_row_costs", "sfrt_multi_balance",
 )
 
 SFRT_MULTI_AUTO, SFRT_MULTI_RCCL, SFRT_MULTI_PEER = 0, 1, 2
@@ -119,6 +120,10 @@ def lib() -> ctypes.CDLL:
         "sfrt_world_update_image": ([W, vp, c_int, c_int, c_int, c_int], c_int),
         "sfrt_world_render_band": ([W, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
         "sfrt_world_check": ([W, vp], c_int),
+        "sfrt_world_row_costs": ([W, vp, c_int, P(c_int), P(c_int)], c_int),
+        "sfrt_multi_cost_bands": ([vp, c_int, c_int, c_float, vp, vp], c_int),
+        "sfrt_multi_row_costs": ([vp, vp, c_int], c_int),
+        "sfrt_multi_balance": ([vp, c_float], c_int),
         "sfrt_world_trace_points": ([W, vp, c_int, vp], c_int),
         "sfrt_world_set_option": ([W, c_int, c_int], c_int),
         "sfrt_world_submit_frame": ([W, vp, P(ctypes.c_int64)], c_int),
@@ -374,6 +379,15 @@ class World:
     def check(self, stream: int = 0) -> None:
         _check(lib().sfrt_world_check(self._h, ctypes.c_void_p(stream or None)), "check")
 
+    def row_costs(self) -> tuple[int, np.ndarray]:
+        """(row0, per-row ray-steps) of the last ordered frame fill (sfrt_world_row_costs)."""
+        _, h = self.size
+        out = np.zeros(max(h, 1), dtype=np.float32)
+        r0, n = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sfrt_world_row_costs(self._h, out.ctypes.data, out.size, ctypes.byref(r0),
+                                          ctypes.byref(n)), "row_costs")
+        return r0.value, out[:n.value].copy()
+
     def trace_points(self, ij) -> list[dict]:
         ij = np.ascontiguousarray(np.asarray(ij, dtype=np.int32).reshape(-1, 2))
         out = (PixelDump * ij.shape[0])()
@@ -477,6 +491,17 @@ def multi_bands(height: int, n: int, root_factor: float = 1.0) -> list[tuple[int
     return [(int(a), int(b)) for a, b in zip(row0, rows)]
 
 
+def multi_cost_bands(row_cost, n: int, root_factor: float = 1.0) -> list[tuple[int, int]]:
+    """sfrt_multi_cost_bands: (row0, rows) per rank, rank 0 ~root_factor x the others' cost."""
+    c = np.ascontiguousarray(np.asarray(row_cost, dtype=np.float32))
+    row0 = np.zeros(n, dtype=np.int32)
+    rows = np.zeros(n, dtype=np.int32)
+    _check(lib().sfrt_multi_cost_bands(c.ctypes.data if c.size else None, int(c.size), int(n),
+                                       float(root_factor), row0.ctypes.data, rows.ctypes.data),
+           "sfrt_multi_cost_bands")
+    return [(int(a), int(b)) for a, b in zip(row0, rows)]
+
+
 class Multi:
     """One frame over several GPUs of this node through the C ABI (sfrt_multi_*): the scene
     setters of ``World`` broadcast to one world per device, the frame is rendered in row
@@ -544,6 +569,26 @@ class Multi:
             return
         r = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
         _check(lib().sfrt_multi_set_bands(self._h, r.ctypes.data, r.size), "multi_set_bands")
+
+    def row_costs(self) -> np.ndarray:
+        """Per-row ray-steps of the last frame, from every rank's band (sfrt_multi_row_costs)."""
+        out = np.zeros(self.height, dtype=np.float32)
+        _check(lib().sfrt_multi_row_costs(self._h, out.ctypes.data, self.height), "multi_row_costs")
+        return out
+
+    def band_costs(self, rank: int) -> tuple[int, np.ndarray]:
+        """(row0, per-row ray-steps) of rank `rank`'s last band (its world's row costs)."""
+        wh = ctypes.c_void_p()
+        _check(lib().sfrt_multi_world(self._h, int(rank), ctypes.byref(wh)), "multi_world")
+        out = np.zeros(max(self.height, 1), dtype=np.float32)
+        r0, n = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sfrt_world_row_costs(wh, out.ctypes.data, out.size, ctypes.byref(r0),
+                                          ctypes.byref(n)), "row_costs")
+        return r0.value, out[:n.value].copy()
+
+    def balance(self, root_factor: float = 1.0) -> None:
+        """Cost-weighted bands from the last frame (sfrt_multi_balance)."""
+        _check(lib().sfrt_multi_balance(self._h, float(root_factor)), "multi_balance")
 
     def render(self, dev_ptr: int, pitch_bytes: int, stream: int = 0) -> None:
         _check(lib().sfrt_multi_render(self._h, ctypes.c_void_p(dev_ptr), int(pitch_bytes),

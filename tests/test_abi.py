@@ -146,6 +146,50 @@ def test_multi_bands_match_band_tuner(lib):
         sfrt.multi_bands(100, 2, float("nan"))
 
 
+def test_multi_cost_bands_match_band_tuner(lib):
+    """sfrt_multi_cost_bands (cost-weighted band edges, SURVEY 8e "Balance") equals
+    bands.cost_weighted_spans row for row; the bands tile the frame on 8-row edges, give
+    rank 0 about `factor` shares of the cost, and fall back to the row-weighted split for
+    costs that carry no information."""
+    import bands
+    import sfrt
+    rng = np.random.default_rng(7)
+    for world_size in (1, 2, 3, 4, 8):
+        for height in (0, 1, 7, 90, 1080, 2160, 4320):
+            for kind in ("random", "uniform", "ramp", "spike"):
+                if kind == "random":
+                    cost = rng.gamma(2.0, 50.0, height).astype(np.float32)
+                elif kind == "uniform":
+                    cost = np.full(height, 3840.0, np.float32)
+                elif kind == "ramp":
+                    cost = np.linspace(1.0, 100.0, height, dtype=np.float32)
+                else:
+                    cost = np.ones(height, np.float32)
+                    cost[height // 3: height // 3 + 8] = 1e4
+                for factor in (1.0, 1.5, 2.0, 3.0, 0.5):
+                    got = sfrt.multi_cost_bands(cost, world_size, factor)
+                    assert got == bands.cost_weighted_spans(cost, world_size, factor), \
+                        (height, world_size, kind, factor)
+                    bands.check_spans(got, height)
+                    assert all(r0 % bands.ALIGN == 0 or r0 == height for r0, _ in got)
+    # balance: equal cost shares within one tile row's cost of the target
+    cost = np.concatenate([np.full(2000, 10.0), np.full(2320, 100.0)]).astype(np.float32)
+    spans = sfrt.multi_cost_bands(cost, 4, 1.0)
+    share = [float(cost[r0:r0 + n].sum()) for r0, n in spans]
+    assert max(share) - min(share) <= 2 * 8 * 100.0, (spans, share)
+    assert spans[0][1] > spans[3][1]  # the cheap rows go to fewer ranks
+    spans2 = sfrt.multi_cost_bands(cost, 4, 2.0)
+    s2 = [float(cost[r0:r0 + n].sum()) for r0, n in spans2]
+    assert abs(s2[0] / s2[1] - 2.0) < 0.1, s2
+    # no information -> the row-weighted split
+    for bad in (np.zeros(4320, np.float32), np.full(4320, -1.0, np.float32),
+                np.full(4320, np.nan, np.float32)):
+        assert sfrt.multi_cost_bands(bad, 4, 2.0) == sfrt.multi_bands(4320, 4, 2.0)
+        assert bands.cost_weighted_spans(bad, 4, 2.0) == bands.root_weighted_spans(4320, 4, 2.0)
+    with pytest.raises(sfrt.SfrtError):
+        sfrt.multi_cost_bands(cost, 0, 1.0)
+
+
 def test_multi_create_without_gpu_fails_loudly(lib):
     import sfrt
     import torch

@@ -100,9 +100,9 @@ def _tune_worker(rank, world_size, port, out_path):
                    .to(torch.uint8)[:, None].expand(rows, pitch))
         time.sleep(1e-4 * rows if rank == 0 else 1e-5 * rows)
 
-    spans, factor, table = bands.tune_spans(render, rank, world_size, height, pitch, "cpu",
-                                            factors=(1.0, 2.0, 3.0), frames=3, warm=1)
-    got = torch.tensor([factor] + [float(n) for _, n in spans], dtype=torch.float64)
+    spans, pick, table = bands.tune_spans(render, rank, world_size, height, pitch, "cpu",
+                                          factors=(1.0, 2.0, 3.0), frames=3, warm=1)
+    got = torch.tensor([pick["root_factor"]] + [float(n) for _, n in spans], dtype=torch.float64)
     allv = [torch.zeros_like(got) for _ in range(world_size)]
     dist.all_gather(allv, got)
     pipe = bands.BandPipeline(rank, world_size, height, pitch, "cpu", spans=spans)

@@ -57,7 +57,21 @@ def _band_worker(rank, world_size, port, key, factor, frames, out_path):
     w = sfrt.World(0)
     w.load_texture(*sc.load_floor())
     w.set_scene(sc.SCENES[g["scene"]]().posed(*g["pose"]), width, height)
-    spans = bands.root_weighted_spans(height, world_size, factor)
+    if isinstance(factor, str):  # "cost:f": cost-weighted bands from an equal-band frame
+        f = float(factor.split(":")[1])
+        r0, n = bands.band_of(rank, world_size, height)
+        tmp = torch.empty(n, pitch, dtype=torch.uint8, device="cuda:0")
+        w.render_band(tmp.data_ptr(), pitch, r0, n, stream.cuda_stream)
+        c0, cost = w.row_costs()
+        assert (c0, cost.size) == (r0, n)
+        full = torch.zeros(height, dtype=torch.float64)
+        full[c0:c0 + n] = torch.from_numpy(cost.astype(np.float64))
+        dist.all_reduce(full)
+        spans = bands.cost_weighted_spans(full.numpy().astype(np.float32), world_size, f)
+        assert spans == sfrt.multi_cost_bands(full.numpy().astype(np.float32), world_size, f)
+        del tmp
+    else:
+        spans = bands.root_weighted_spans(height, world_size, factor)
     pipe = bands.BandPipeline(rank, world_size, height, pitch, "cpu", spans=spans)
     dev = torch.empty(max(pipe.rows, 1), pitch, dtype=torch.uint8, device="cuda:0")
     for k in range(frames):
@@ -80,6 +94,7 @@ def _band_worker(rank, world_size, port, key, factor, frames, out_path):
     ("c4_7680x4320_lcg64@0,0", 2, 1.0), ("c4_7680x4320_lcg64@0,0", 4, 1.0),
     ("c4_7680x4320_default10@0,0", 2, 1.0), ("c4_7680x4320_default10@0,0", 4, 1.0),
     ("c4_7680x4320_lcg64@0,0", 2, 2.5), ("c4_7680x4320_default10@0,0", 4, 2.0),
+    ("c4_7680x4320_lcg64@0,0", 4, "cost:1.0"), ("c4_7680x4320_default10@0,0", 2, "cost:2.0"),
     ("c5_16384x16384_default10@0,0", 8, 1.0)])
 def test_distributed_bands_match_golden(tmp_path, key, world_size, factor):
     """world_size ranks on cuda:0, HIP-rendered bands, gathered to rank 0 by BandPipeline
@@ -172,3 +187,91 @@ def test_multi_render_pipelined_frames(floor_tex, n, transport):
         torch.cuda.synchronize()
         for k, f in enumerate(frames):
             assert np.array_equal(f.cpu().numpy().ravel(), want[k]), k
+
+
+def _class_steps(cls):
+    """Host restatement of sfrt_world.cpp class_steps (the inverse of tile_bucket)."""
+    c = 15 - cls
+    if c == 0:
+        return 3.0
+    if c <= 6:
+        return 2.0 * c + 2.5
+    if c <= 10:
+        return 16.0 + 4.0 * (c - 7) + 1.5
+    return (35.5, 43.5, 55.5, 79.5, 128.0)[c - 11]
+
+
+def _bucket(steps):
+    """sfrt_device.h tile_bucket."""
+    c = (0 if steps < 4 else (steps - 2) >> 1) if steps < 16 else \
+        7 + ((steps - 16) >> 2) if steps < 32 else \
+        11 if steps < 40 else 12 if steps < 48 else 13 if steps < 64 else 14 if steps < 96 else 15
+    return 15 - c
+
+
+def _expected_row_costs(iters, width, row0, rows):
+    """Row costs of an ordered band [row0, row0 + rows): each tile (R*8 x 8, R from the
+    kernel table's rule) costs its slowest ray's march steps (class midpoint) + 4."""
+    ty_n = (rows + 7) // 8
+    t4 = ((width + 31) // 32) * ty_n
+    t3 = ((width + 23) // 24) * ty_n
+    tw = 32 if t4 >= 30000 else 24 if t3 >= 30000 else 16
+    out = np.zeros(rows, np.float64)
+    band = iters[row0:row0 + rows]
+    for ty in range(ty_n):
+        rr = band[ty * 8:(ty + 1) * 8]
+        c = 0.0
+        for x0 in range(0, width, tw):
+            steps = int(rr[:, x0:x0 + tw].max())
+            c += (_class_steps(_bucket(steps)) + 4.0) * min(tw, width - x0)
+        out[ty * 8:(ty + 1) * 8] = c
+    return out.astype(np.float32)
+
+
+@pytest.mark.parametrize("name,width,height,pose,row0,rows", [
+    ("default10", 1920, 1080, (0.0, 0.0), 0, 1080),
+    ("lcg64", 3840, 2160, (0.0, 0.0), 0, 2160),
+    ("lcg64", 3840, 2160, (1.1, -0.2), 1000, 1160)])
+def test_row_costs_equal_oracle_march_steps(floor_tex, name, width, height, pose, row0, rows):
+    """sfrt_world_row_costs after an ordered render_band: every tile's recorded class is
+    the class of its slowest ray's march steps in the oracle (iteration_map), so the row
+    costs equal the host computation from the oracle exactly."""
+    import oracle
+    import sfrt
+    import torch
+    from conftest import host_threads
+    sc = scenes.SCENES[name]().posed(*pose)
+    it = oracle.Oracle.from_scene(sc, width, height, *floor_tex).iteration_map(host_threads())
+    it = it.reshape(height, width)
+    w = sfrt.World(0)
+    w.load_texture(*floor_tex)
+    w.set_scene(sc, width, height)
+    buf = torch.empty(rows, width * 4, dtype=torch.uint8, device="cuda")
+    for _ in range(3):  # first launch records, later ones also run in the adaptive order
+        w.render_band(buf.data_ptr(), width * 4, row0, rows)
+    r0, cost = w.row_costs()
+    w.check()
+    assert r0 == row0 and cost.size == rows
+    np.testing.assert_array_equal(cost, _expected_row_costs(it, width, row0, rows))
+    w.close()
+
+
+@pytest.mark.parametrize("key,n,factor", [
+    ("c4_7680x4320_lcg64@0,0", 4, 1.0), ("c4_7680x4320_default10@0,0", 2, 2.0)])
+def test_multi_balance_matches_golden(floor_tex, key, n, factor):
+    """sfrt_multi_balance: cost-weighted bands from the last frame's row costs (every row
+    covered by some rank's band), then the frame again -- still the golden bytes."""
+    import oracle
+    import sfrt
+    g = GOLDEN["frames"][key]
+    with _multi([0] * n, sfrt.SFRT_MULTI_PEER, floor_tex) as m:
+        m.set_scene(scenes.SCENES[g["scene"]]().posed(*g["pose"]), g["width"], g["height"])
+        first = m.update_image()
+        cost = m.row_costs()
+        assert cost.size == g["height"] and (cost > 0).all()
+        want = sfrt.multi_cost_bands(cost, n, factor)
+        m.balance(factor)
+        assert oracle.fnv1a64(m.update_image()) == g["fnv1a64"] == oracle.fnv1a64(first)
+        # the partition sfrt_multi used is the cost-weighted one: its ranks' last bands
+        got = [m.band_costs(r) for r in range(n)]
+        assert [(r0, c.size) for r0, c in got] == want
