@@ -27,7 +27,9 @@
 
 // Diagnostic builds only (tools/ab_libs.py, tools/tile_timeline.py), never the shipped
 // library: -DSFRT_EXP=16 writes per-tile wall-clock start/end into each tile's first
-// pixels, -DSFRT_EXP=64 skips the shading tail (timing probes; both write wrong bytes).
+// pixels, -DSFRT_EXP=32 per-tile march counters (steps, sphere visits, visits that
+// passed for some ray, window/slot mode, culled spheres; tools/visit_counts.py),
+// -DSFRT_EXP=64 skips the shading tail (timing probes; all write wrong bytes).
 #ifndef SFRT_EXP
 #define SFRT_EXP 0
 #endif
@@ -292,7 +294,7 @@ __device__ __forceinline__ void zero_steps(float (&L)[R]) {
 // rad > 2^-7, and rad - q == rad for any q < 2^-33, which both roots of such
 // ss are (tests/native/wave_check.hip, every ss).
 template <int R>
-__device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, float rad, int k,
+__device__ __forceinline__ bool pass_body_r(const float (&ss)[R], float s_pass, float rad, int k,
                                             float (&L)[R], int (&draw)[R]) {
   uint64_t any = 0;
 #pragma unroll
@@ -308,6 +310,7 @@ __device__ __forceinline__ void pass_body_r(const float (&ss)[R], float s_pass, 
       }
     }
   }
+  return any != 0;
 }
 
 // The march (SphereWorld.cpp:359-372), one wave per (8R)x8 tile.  Lane l holds
@@ -441,11 +444,19 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       tacc[r] = tacc[r] + L[r];
     }
   };
+#if SFRT_EXP & 32  // diagnostic build: per-tile visit counters (wrong bytes)
+  uint32_t dbg_visits = 0, dbg_passes = 0, dbg_mode = 0;
+#endif
   auto visit = [&](float cx, float cy, float cz, float rad, float s_pass, int k, float (&L)[R]) {
     float ss[R];
 #pragma unroll
     for (int r = 0; r < R; r++) ss[r] = dist2(px[r], py[r], pz[r], cx, cy, cz);
+#if SFRT_EXP & 32
+    dbg_visits++;
+    dbg_passes += pass_body_r<R>(ss, s_pass, rad, k, L, draw) ? 1u : 0u;
+#else
     pass_body_r<R>(ss, s_pass, rad, k, L, draw);
+#endif
   };
   // Every sphere in index order (no culling: cull off, or past kCullSafeIterations steps).
   auto visit_all = [&](float (&L)[R]) {
@@ -493,6 +504,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       advance(L);
     }
   } else {
+#if SFRT_EXP & 32
+    dbg_mode = 1;
+#endif
     float tlo = 0.0f;
     for (; any_marching() && trips < cull_end; ++trips) {
       float L[R];
@@ -581,6 +595,13 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       if (sh[r].outside) atomicOr(f.status, 2);  // the reference would read outside the image
       *px_out(r) = shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
     }
+  }
+#endif
+#if SFRT_EXP & 32
+  if (lane_s < 5 && valid(0)) {
+    const uint32_t v = lane_s == 0 ? (uint32_t)trips : lane_s == 1 ? dbg_visits : lane_s == 2 ? dbg_passes
+                     : lane_s == 3 ? dbg_mode : (uint32_t)__builtin_popcountll(m);
+    *px_out(0) = v;
   }
 #endif
 #if SFRT_EXP & 16
