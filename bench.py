@@ -151,16 +151,18 @@ def settle(world, pitch, row0, rows, stream, seconds: float) -> None:
     del buf
 
 
-def frame_row_costs(world, rank, world_size, height, pitch, stream):
+def frame_row_costs(world, rank, world_size, height, pitch, stream, device="cuda"):
     """The frame's per-row work (sfrt_world_row_costs) on every rank: each rank renders its
     equal band once in the adaptive tile order, and the bands' costs are summed over ranks
     into one full-height vector (SURVEY 8e "Balance": cost-weighted band edges)."""
     r0, n = band_of(rank, world_size, height)
-    buf = torch.empty(max(n, 1), pitch, dtype=torch.uint8, device="cuda")
+    buf = torch.empty(max(n, 1), pitch, dtype=torch.uint8, device=device)
     world.render_band(buf.data_ptr(), pitch, r0, n, stream.cuda_stream)
     c0, cost = world.row_costs()
-    full = torch.zeros(height, dtype=torch.float64, device="cuda")
-    full[c0:c0 + cost.size] = torch.from_numpy(cost.astype(np.float64)).to("cuda")
+    if (c0, cost.size) != (r0, n):
+        raise RuntimeError(f"row costs cover rows {c0}+{cost.size}, the band is {r0}+{n}")
+    full = torch.zeros(height, dtype=torch.float64, device=device)
+    full[c0:c0 + cost.size] = torch.from_numpy(cost.astype(np.float64)).to(device)
     dist.all_reduce(full)
     del buf
     return full.cpu().numpy().astype(np.float32)

@@ -121,3 +121,47 @@ def test_tune_spans_agrees_across_ranks(tmp_path):
     mp.start_processes(_tune_worker, args=(3, _free_port(), out), nprocs=3,
                        start_method="spawn", join=True)
     assert np.load(out).all()
+
+
+def _row_cost_worker(rank, world_size, port, out_path):
+    import sys
+    for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), ROOT):
+        sys.path.insert(0, p)
+    import types
+    import bands
+    import bench
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world_size)
+    height, pitch = 100, 16
+    calls = []
+
+    class FakeWorld:  # stands in for sfrt.World: row j of the frame costs j + 1
+        def render_band(self, ptr, p, row0, rows, stream):
+            calls.append((row0, rows))
+
+        def row_costs(self):
+            row0, rows = calls[-1]
+            return row0, np.arange(row0 + 1, row0 + rows + 1, dtype=np.float32)
+
+    cost = bench.frame_row_costs(FakeWorld(), rank, world_size, height, pitch,
+                                 types.SimpleNamespace(cuda_stream=0), device="cpu")
+    ok = [calls == [bands.band_of(rank, world_size, height)],
+          bool(np.array_equal(cost, np.arange(1, height + 1, dtype=np.float32)))]
+    spans = bands.cost_weighted_spans(cost, world_size, 1.0)
+    got = torch.tensor([float(n) for _, n in spans], dtype=torch.float64)
+    allv = [torch.zeros_like(got) for _ in range(world_size)]
+    dist.all_gather(allv, got)
+    ok.append(all(torch.equal(a, allv[0]) for a in allv))
+    if rank == 0:
+        np.save(out_path, np.array(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_row_costs_sum_over_ranks(tmp_path):
+    """bench.frame_row_costs: every rank renders its equal band once and the ranks' row costs
+    add up to the whole frame's vector (the cost-weighted band tuner's input at N > 1)."""
+    out = str(tmp_path / "rc.npy")
+    mp.start_processes(_row_cost_worker, args=(3, _free_port(), out), nprocs=3,
+                       start_method="spawn", join=True)
+    assert np.load(out).all()
