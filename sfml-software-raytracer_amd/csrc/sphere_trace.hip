@@ -518,7 +518,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         const uint32_t u = __float_as_uint(tacc[r]);
         th = u > th ? u : th;
       }
-      if (trips % 2 == 1) {  // the low end, every second step
+      if (trips % 2 == 1) {  // the low end, every second step (every 3rd/4th: slower)
         uint32_t tl = 0x7f800000u;  // +inf
 #pragma unroll
         for (int r = 0; r < R; r++) {
