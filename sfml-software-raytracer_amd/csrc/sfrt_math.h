@@ -166,6 +166,22 @@ SFRT_HD float asinf_tail_div(float a, float b) {
 #endif
 }
 
+// sqrtf(t) for e_asinf.c's t = (1 - |x|) / 2 in [2^-25, 0.25]: on the device the raw
+// v_sqrt_f32 corrected by the compiler's own two fma residual tests, without its rescaling
+// for arguments below 2^-96 and its special-value selects, which such t never need (the
+// same sequence as sfrt_device.h sqrt_cr_normal); `sqrtf` elsewhere.  Same bits.
+SFRT_HD float asinf_sqrt(float t) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float r = __builtin_amdgcn_sqrtf(t);
+  const float rm = u2f(f2u(r) - 1u), rp = u2f(f2u(r) + 1u);
+  float q = __builtin_fmaf(-rm, r, t) <= 0.0f ? rm : r;
+  q = __builtin_fmaf(-rp, r, t) > 0.0f ? rp : q;
+  return q;
+#else
+  return __builtin_sqrtf(t);
+#endif
+}
+
 // e_asinf.c
 SFRT_HD float asinf(float x) {
   const float pio2_hi = u2f(0x3fc90fdbu);
@@ -186,7 +202,7 @@ SFRT_HD float asinf(float x) {
   const float w = 1.0f - u2f(ix);
   const float t = w * 0.5f;
   const float p = ((((p4 * t + p3) * t + p2) * t + p1) * t + p0) * t;
-  const float s = __builtin_sqrtf(t);
+  const float s = asinf_sqrt(t);
   float r;
   if (ix >= 0x3f79999au) {                                // |x| > 0.975
     const float q = s * p + s;
