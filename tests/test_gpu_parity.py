@@ -551,3 +551,39 @@ def test_adaptive_order_ragged_wide_tiles(world, floor, width, height):
     sc = scenes.lcg64().posed(*poses[1])
     assert diff_report(want[poses[1]], oracle_for(sc, width, height, floor).render(host_threads()),
                        width) == ""
+
+
+def _division_guard_scenes():
+    """Scenes whose pixels leave div_inrange's operand range ("Divisions without
+    range scaling"), so that their waves take the compiler's full division: 256 x 256 frames
+    with a power-of-two field of view (h_inc = v_inc = 2^-8) and the camera on the z axis:
+    column 128's primary rays have x == +0 (primary_dir's guard), their hit points px == 0
+    (atan2f_wave's general path), and row 128's hit points ey == 0 (the asinf argument's
+    division).  (Scenes scaled far enough for |p - cam| >= 2^40 do not converge: the
+    reference's march never ends once a step is below half an ulp of the position.)"""
+    one = scenes.Scene("origin", np.array([[0, 0, 0, 4]], np.float32), cam_pos=(0.0, 0.0, 0.0),
+                       fov_h=0.5, fov_v=0.5)
+    two = scenes.Scene("axis2", np.array([[0, 0, 0, 4], [0, 0, 3, 2.5], [0, 0, -3, 1.5]],
+                                         np.float32), cam_pos=(0.0, 0.0, 0.5), fov_h=1.0, fov_v=0.5)
+    return [(one, 256, 256), (two, 256, 256), (two, 512, 256), (one.posed(0.3, 0.0), 256, 256)]
+
+
+@pytest.mark.parametrize("case", range(4))
+def test_division_guard_paths_match_oracle(world, floor, case):
+    """Frames whose waves take the general division / atan2 paths equal the oracle's, through
+    update_image (row-major, 8x8 / 16x8 tiles) and ordered render_band frames (the kernel
+    table's choice, four back to back)."""
+    import sfrt
+    import torch
+    sc, width, height = _division_guard_scenes()[case]
+    world.set_scene(sc, width, height)
+    want = oracle_for(sc, width, height, floor).render(host_threads())
+    assert diff_report(world.render(), want, width) == ""
+    for rays in (0, 4):  # 0: the kernel table's pick; 4: 32x8 tiles
+        world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
+        b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        for _ in range(4):
+            world.render_band(b.data_ptr(), width * 4, 0, height)
+        world.check()
+        assert diff_report(b.cpu().numpy().ravel(), want, width) == "", rays
+    world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
