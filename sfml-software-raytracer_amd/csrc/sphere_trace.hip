@@ -2,13 +2,15 @@
 //
 // Replaces the per-pixel body of SphereWorld::UpdateImage / Raycast
 // (/root/reference/Raytracing/SphereWorld.cpp:83-112, 355-382): one wave64 per
-// (8R)x8 pixel tile, R = 1..4 pixels per lane (n <= 64 spheres; 8x8 tiles in
-// four-wave workgroups above that), RGBA8 written straight to HBM.
+// (8R)x8 pixel tile, R = 1..4 pixels per lane (records in the kernel arguments for
+// n <= 64 spheres, a per-wave culled list above that), RGBA8 written straight to HBM.
 //
 // Bit-exactness rules (see DESIGN.md "Exactness"):
 //  * built with -ffp-contract=off; every float expression keeps the
 //    reference's operand order; division and sqrt are the correctly rounded
-//    gfx950 sequences (hipcc default);
+//    gfx950 sequences (hipcc default), or the same sequences without their
+//    range scaling where the operands provably need none (div_inrange,
+//    sqrt_cr_normal: sfrt_device.h);
 //  * atan2f / asinf are sfrt_math:: restatements of the host libm;
 //  * the sphere test `r - sqrtf(s) > 0.01f` is replaced by `s < s_pass`, where
 //    s_pass is the exact binary32 threshold found on the host (the test is
@@ -472,11 +474,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   // or a full/culled branch inside the step, makes the compiler copy every loop-carried
   // register (draw, L) between register sets each step.
   const int cull_end = full ? 1 : kCullSafeIterations;
-#ifdef SFRT_SLOTS
-  constexpr int kSlotsR = SFRT_SLOTS;
-#else
   constexpr int kSlotsR = kSlots;
-#endif
   if (kSlotsR > 0 && !full && __builtin_popcountll(m) <= kSlotsR) {
     constexpr int NS = kSlotsR > 0 ? kSlotsR : 1;
     // Few culled spheres: hold them in SGPR slots and test every one each step
@@ -614,21 +612,17 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 #endif
 }
 
-// n <= 64: the records travel in the kernel-argument segment.
+// n <= 64: the records travel in the kernel-argument segment.  8 waves/SIMD: <= 64
+// VGPRs (R = 4 needs 60; measured equal to 7 waves when it spilled one, ab/r2_ab10).
 template <int R>
-#ifndef SFRT_R_WAVES
-#define SFRT_R_WAVES 8
-#endif
-__global__ __launch_bounds__(64, SFRT_R_WAVES) void k_trace_window_r(InlineArgs args) {
+__global__ __launch_bounds__(64, 8) void k_trace_window_r(InlineArgs args) {
   trace_tile_window_r<R, false>(args.f, args.s);
 }
 
-// n > 64: the records in device memory (f.spheres), the culled list per wave.
+// n > 64: the records in device memory (f.spheres), the culled list per wave.  66
+// VGPRs at R = 4 (7 waves/SIMD; forcing 8 spilled two and gained nothing, ab/r2_ab12).
 template <int R>
-#ifndef SFRT_LIST_WAVES
-#define SFRT_LIST_WAVES 1
-#endif
-__global__ __launch_bounds__(64, SFRT_LIST_WAVES) void k_trace_window_list(FrameRec f) {
+__global__ __launch_bounds__(64) void k_trace_window_list(FrameRec f) {
   trace_tile_window_r<R, true>(f, f.spheres);
 }
 
