@@ -8,7 +8,7 @@
 // GL_NEAREST_MIPMAP_LINEAR sampling of the mipmapped REPEAT `ground`, unorm8
 // framebuffer rounding) and this kernel is held to the CPU restatement
 // (oracle/glsl_oracle.c) bit for bit.  Every expression keeps the shader's
-// operand order.  Sphere data are wave-uniform (scalar loads); only the
+// operand order.  Sphere data are read at wave-uniform addresses; only the
 // per-fragment lookups by drawSphere (:123-125, :154) are vector loads.
 #include <hip/hip_runtime.h>
 
@@ -244,9 +244,10 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
         unorm8(cr) | (unorm8(cg) << 8) | (unorm8(cbl) << 16) | (255u << 24);
 }
 
-// Wall and ball records are read once per visit by every wave, with scalar
-// loads (wave-uniform addresses, scalar cache); staging them in LDS measured
-// 5-10% slower (profiles/r1_glsl_variants.json).  Four 8x8 tiles (one per
+// Wall and ball records are read once per visit by every wave at wave-uniform
+// addresses; staging them in LDS measured 5-10% slower (profiles/r1_glsl_variants.json),
+// scalar loads through the constant address space or a next-record prefetch 7-8%
+// slower (profiles/ab/r2_ab18).  Four 8x8 tiles (one per
 // wave) per 256-thread workgroup, row-major.
 __global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
   const int lane = threadIdx.x & 63;
