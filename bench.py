@@ -262,6 +262,9 @@ def main() -> None:
                     help="seconds of untimed frames before the warm-up (clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the 8K / 16K frames")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the headline workload (no also lines, no CPU baseline): the command "
+                         "whose rocprof kernel trace profiles/*_kernel_stats_by_grid.csv summarises")
     args = ap.parse_args()
 
     if not torch.cuda.is_available():
@@ -352,14 +355,14 @@ def main() -> None:
     # Larger frames of the BASELINE configs (strong scaling: the frame is fixed,
     # its rows split over the ranks), measured after the main line.
     extra = {}
-    if not args.no_extra:
+    if not (args.no_extra or args.headline_only):
         for fw, fh in EXTRA_FRAMES.get(world_size, []):
             extra[f"{fw}x{fh}_lcg64"] = measure_frame(w, scene, fw, fh, rank, world_size,
                                                       max(5, args.steps // 2), 2, stream)
         w.set_scene(scene, WIDTH, height)
     if rank == 0:
         result["also"] = dict(extra)
-    if world_size == 1:
+    if world_size == 1 and not args.headline_only:
         # BASELINE config 2: 1920x1080, 10-sphere scene.
         w2 = sfrt.World(local_rank)
         w2.load_texture(*floor)

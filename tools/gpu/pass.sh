@@ -14,5 +14,5 @@ grep -q "failed\|Fatal\|core dumped\|Timeout" $O/gpu_tests.log && exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
-  python bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-extra > $O/bench_trace.json 2> $O/bench_trace.err || exit 1
+  python bench.py --steps 100 --warmup 20 --no-cpu-baseline --headline-only > $O/bench_trace.json 2> $O/bench_trace.err || exit 1
 echo done

@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-prof}
 mkdir -p $O
-B="bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra"
+B="bench.py --steps 20 --warmup 3 --no-cpu-baseline --headline-only"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python $B > $O/bench_trace.json 2> $O/trace.err || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python $B > $O/pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python $B > $O/pmc_write.log 2>&1 || exit 1
