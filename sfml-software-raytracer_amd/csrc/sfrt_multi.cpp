@@ -141,6 +141,7 @@ struct sfrt_multi {
   std::vector<Rank> ranks;
   int transport = SFRT_MULTI_PEER;
   std::vector<int> rows_set;  // sfrt_multi_set_bands (empty: equal split)
+  std::vector<int> last_rows; // the bands of the last render (sfrt_multi_row_costs)
   int64_t k = 0;              // frames rendered (band buffer k % 2)
   hipEvent_t start = nullptr;  // on devices[0]: the caller's stream position at render
   hipStream_t out_s = nullptr;  // devices[0]: update_image's frame stream
@@ -212,6 +213,7 @@ struct sfrt_multi {
     if (pitch != (int64_t)width * 4) return SFRT_E_INVALID;  // bands are contiguous rows
     std::vector<int> row0, rows;
     if ((rc = spans(height, row0, rows))) return rc;
+    last_rows = rows;
     const int n = (int)ranks.size();
     bool equal = true;
     for (int r = 1; r < n; r++) equal = equal && rows[r] == rows[0];
@@ -471,7 +473,9 @@ int sfrt_multi_row_costs(sfrt_multi* m, float* costs, int height) {
   if (!m || height < 0 || (height > 0 && !costs)) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(m->mu);
   std::vector<char> seen((size_t)height, 0);
-  for (auto& R : m->ranks) {
+  for (size_t q = 0; q < m->ranks.size(); q++) {
+    auto& R = m->ranks[q];
+    if (q < m->last_rows.size() && m->last_rows[q] == 0) continue;  // rendered nothing
     int r0 = 0, nr = 0, w = 0, h = 0;
     int rc = sfrt_world_get_size(R.world, &w, &h);
     if (rc) return rc;

@@ -688,7 +688,10 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   int rc = w->validate();
   if (rc) return rc;
   if (pitch_bytes < (int64_t)w->width * 4 || row0 + rows > w->height) return SFRT_E_INVALID;
-  if (rows == 0) return SFRT_OK;
+  if (rows == 0) {
+    w->last_fill.valid = false;  // the last fill covered no rows (sfrt_world_row_costs)
+    return SFRT_OK;
+  }
   sfrt::DeviceGuard g(w->device);
   hipStream_t s = (hipStream_t)hip_stream;  // HIP convention: NULL = the null stream
   sfrt::FrameRec f;

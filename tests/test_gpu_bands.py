@@ -275,3 +275,28 @@ def test_multi_balance_matches_golden(floor_tex, key, n, factor):
         # the partition sfrt_multi used is the cost-weighted one: its ranks' last bands
         got = [m.band_costs(r) for r in range(n)]
         assert [(r0, c.size) for r0, c in got] == want
+
+
+def test_multi_row_costs_skip_empty_bands(floor_tex):
+    """A rank whose band is empty renders nothing and is skipped: with bands [H, 0] the
+    frame's row costs are rank 0's, equal to one world's row costs of the whole frame."""
+    import sfrt
+    import torch
+    g = GOLDEN["frames"]["c4_7680x4320_lcg64@0,0"]
+    sc = scenes.SCENES[g["scene"]]().posed(*g["pose"])
+    with _multi([0, 0], sfrt.SFRT_MULTI_PEER, floor_tex) as m:
+        m.set_scene(sc, g["width"], g["height"])
+        m.set_bands([g["height"], 0])
+        m.update_image()
+        cost = m.row_costs()
+        assert m.band_costs(0)[0] == 0
+    w = sfrt.World(0)
+    w.load_texture(*floor_tex)
+    w.set_scene(sc, g["width"], g["height"])
+    buf = torch.empty(g["height"], g["width"] * 4, dtype=torch.uint8, device="cuda")
+    w.render_band(buf.data_ptr(), g["width"] * 4, 0, g["height"])
+    r0, want = w.row_costs()
+    w.check()
+    w.close()
+    assert r0 == 0
+    np.testing.assert_array_equal(cost, want)
