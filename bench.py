@@ -13,6 +13,9 @@ whose band never crosses a link, may take more rows).  Per-GPU work is fixed
 on average as N grows ("weak" scaling); rays use the global row index, so the
 gathered frame is byte-identical to a single-GPU render of the same frame.
 value = all rays of the K frames / (max over ranks of the timed wall time).
+One frame at a time on one stream; at N = 1 the `*_2_in_flight` lines under "also" render
+frames alternately on two HIP streams into two buffers, frame k+1 starting while frame k's
+last tiles drain (the throughput of a double-buffered display or offline loop).
 Before the W warm-up frames, --settle seconds of untimed frames let the chip
 reach its steady clock (it ramps over the first few hundred frames).
 
@@ -90,19 +93,43 @@ def event_pair_ms(stream, n: int = 64) -> float:
     return float(np.median([a.elapsed_time(b) for a, b in pairs]))
 
 
-def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream, per_frame=None):
-    """Warmup, then `steps` timed frames through the pipeline.  Returns (wall seconds,
-    kernel ms per frame from HIP events around every EVENT_EVERY-th render on the launch
-    stream, minus the empty event pair's own elapsed time).
+# Two frames in flight (the `*_2_in_flight` lines under also, N = 1): frames alternate
+# between the launch stream and a second stream, each into its own buffer, so frame k+1
+# starts while frame k's last tiles drain -- each stream has its own tile-order chain in
+# libsfrt (sfrt_sched.h TileChains).  The headline stays one frame at a time: its kernel_ms is then each launch's
+# own time, as the rocprof trace and the roofline use it (with two in flight every launch
+# shares the chip with the next and its duration says nothing about throughput).
+SECOND_STREAM = []
+
+
+def frame_streams(stream, in_flight: int):
+    if in_flight == 1:
+        return [stream]
+    if not SECOND_STREAM:
+        SECOND_STREAM.append(torch.cuda.Stream())
+    return [stream, SECOND_STREAM[0]]
+
+
+def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream, per_frame=None,
+                in_flight: int = 1):
+    """Warmup, then `steps` timed frames through the pipeline, frame k on
+    streams[k % in_flight] (pipe.depth >= in_flight buffers in turn).  Returns (wall
+    seconds, kernel ms per launch from HIP events around every EVENT_EVERY-th render on its
+    launch stream, minus the empty event pair's own elapsed time).
     per_frame(k), if given, runs before frame k is queued (a moving camera)."""
+    streams = frame_streams(stream, in_flight)
+    if pipe.depth < len(streams):
+        raise ValueError("one frame buffer per stream in flight")
     for k in range(warmup):
         if per_frame:
             per_frame(k)
         world.render_band(pipe.acquire(k).data_ptr(), pitch, pipe.row0, pipe.rows,
-                          stream.cuda_stream)
+                          streams[k % len(streams)].cuda_stream)
         pipe.submit(k)
     pipe.drain()
-    world.check(stream.cuda_stream)
+    torch.cuda.synchronize()
+    for s in streams:
+        world.check(s.cuda_stream)
     # HIP events around every EVENT_EVERY-th frame only: an event is a marker
     # packet in the stream, and one pair per frame would add its own gap to
     # every frame of the wall-clock measurement.
@@ -117,18 +144,20 @@ def time_frames(world, pipe: BandPipeline, pitch, steps, warmup, stream, per_fra
         if per_frame:
             per_frame(warmup + k)
         band = pipe.acquire(k)
+        sk = streams[k % len(streams)]  # frame k's buffer is pipe.acquire(k): k % depth
         if k in starts:
-            starts[k].record(stream)
-        world.render_band(band.data_ptr(), pitch, pipe.row0, pipe.rows, stream.cuda_stream)
+            starts[k].record(sk)
+        world.render_band(band.data_ptr(), pitch, pipe.row0, pipe.rows, sk.cuda_stream)
         if k in ends:
-            ends[k].record(stream)
+            ends[k].record(sk)
         pipe.submit(k)
     pipe.drain()
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     wall = time.perf_counter() - t0
-    world.check(stream.cuda_stream)
+    for s in streams:
+        world.check(s.cuda_stream)
     raw = sum(starts[k].elapsed_time(ends[k]) for k in sampled) / len(sampled)
     kernel_ms = max(0.0, raw - event_pair_ms(stream))
     return wall, kernel_ms
@@ -322,7 +351,8 @@ def main() -> None:
                                       if world_size > 1 else ""),
                        "width": WIDTH, "height": height, "spheres": int(scene.spheres.shape[0]),
                        "camera": "static pose (0,0); moving-camera lines under also",
-                       "parallelism": f"row-bands x{world_size}"},
+                       "parallelism": f"row-bands x{world_size}",
+                       "frames_in_flight": 1},
             "kernel_ms": round(kernel_ms, 4),
             "bands": bands,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -421,6 +451,21 @@ def main() -> None:
             "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4), "spheres": 256}
         w5.close()
         del pipe5
+        # Two frames in flight (see frame_streams): the 4K static and 1080p frames.
+        for key, (fw, fh, sc2) in (("3840x2160_lcg64_2_in_flight", (WIDTH, height, scene)),
+                                   ("1920x1080_default10_2_in_flight", (1920, 1080, scenes.default10()))):
+            w6 = sfrt.World(local_rank)
+            w6.load_texture(*floor)
+            w6.set_scene(sc2, fw, fh)
+            pipe6 = BandPipeline(0, 1, fh, fw * 4, "cuda", local_depth=2)
+            wall6, k6 = time_frames(w6, pipe6, fw * 4, args.steps, args.warmup, stream, in_flight=2)
+            result["also"][key] = {
+                "n_gpus": 1, "Mrays_per_s": round(fw * fh * args.steps / wall6 / 1e6, 2),
+                "fps": round(args.steps / wall6, 2), "ms_per_frame": round(wall6 / args.steps * 1e3, 4),
+                "kernel_ms_per_launch_overlapping": round(k6, 4),
+                "frames_in_flight": 2, "streams": 2}
+            w6.close()
+            del pipe6
         if not args.no_cpu_baseline:
             torch.cuda.synchronize()
             gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()

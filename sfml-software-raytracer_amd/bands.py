@@ -126,18 +126,20 @@ class BandPipeline:
     exchanged."""
 
     def __init__(self, rank: int, world_size: int, height: int, pitch: int, device,
-                 depth: int = 2, spans=None):
+                 depth: int = 2, spans=None, local_depth: int = 1):
         self.rank, self.world_size, self.height = rank, world_size, height
         self.spans = list(spans) if spans is not None else equal_spans(height, world_size)
         check_spans(self.spans, height)
         if len(self.spans) != world_size:
             raise ValueError("one band per rank")
         self.equal = len({n for _, n in self.spans}) == 1
-        self.depth = depth if world_size > 1 else 1
+        # one rank: `local_depth` whole frames (several frames in flight on as many streams)
+        self.depth = depth if world_size > 1 else local_depth
         self.row0, self.rows = self.spans[rank]
         self.frames, self.views = [], []
         if world_size == 1:
-            self.frames = [torch.empty(height, pitch, dtype=torch.uint8, device=device)]
+            self.frames = [torch.empty(height, pitch, dtype=torch.uint8, device=device)
+                           for _ in range(self.depth)]
             self.bands = self.frames
         else:
             if rank == 0:

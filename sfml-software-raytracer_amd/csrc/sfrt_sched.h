@@ -37,6 +37,7 @@ struct TileSched {
   bool committed = false;        // the last end() advanced the chain
   hipStream_t last_stream = nullptr;
   bool have_last = false;
+  uint64_t used = 0;             // TileChains: when the chain last took a launch
 
   void release() {
     for (int q = 0; q < 2; q++) {
@@ -113,6 +114,35 @@ struct TileSched {
     key_prev = 0;
     sorted_prev = false;
     pending_key = 0;
+  }
+};
+
+// One chain per stream (up to kChains streams): launches on different streams share no
+// cost or order buffer, so nothing orders them against each other -- two frames in flight
+// on two streams overlap, the second starting while the first drains.  Each chain orders
+// its launches by the march steps of its own launch two back.  A further stream takes the
+// least recently used chain, whose begin() then waits for that chain's last stream.
+struct TileChains {
+  static constexpr int kChains = 4;
+  TileSched chain[kChains];
+  uint64_t clock = 0;
+
+  int pick(hipStream_t s) {
+    int lru = 0;
+    for (int q = 0; q < kChains; q++)
+      if (chain[q].have_last && chain[q].last_stream == s) return touch(q);
+    for (int q = 0; q < kChains; q++)
+      if (!chain[q].have_last) return touch(q);
+    for (int q = 1; q < kChains; q++)
+      if (chain[q].used < chain[lru].used) lru = q;
+    return touch(lru);
+  }
+  int touch(int q) {
+    chain[q].used = ++clock;
+    return q;
+  }
+  void release() {
+    for (auto& c : chain) c.release();
   }
 };
 

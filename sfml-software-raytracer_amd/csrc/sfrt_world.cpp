@@ -129,7 +129,8 @@ struct sfrt_world {
   uint32_t* d_tex = nullptr;  // texture atlas: every loaded slot, back to back
   size_t d_tex_texels = 0;
   int* d_status = nullptr;
-  sfrt::TileSched sched;  // adaptive tile order (sfrt_sched.h), render_band / submit_frame
+  sfrt::TileChains scheds;  // adaptive tile order (sfrt_sched.h), one chain per stream
+  int cur_chain = 0;        // the chain of the launch between sched_begin and sched_end
   // Device copies of the sphere records for launches that read them from memory
   // (> 64 spheres, trace_points): a ring of slots, each with pinned staging and
   // the event of the last launch that read it, so a slot is never overwritten
@@ -173,7 +174,7 @@ struct sfrt_world {
       if (p.copied) (void)hipEventDestroy(p.copied);
     }
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    sched.release();
+    scheds.release();
     (void)hipFree(d_tex);
     (void)hipFree(d_status);
     (void)hipDeviceSynchronize();
@@ -329,9 +330,13 @@ struct sfrt_world {
     long long tiles = 0;
     const long long key = tile_order_on ? sfrt::trace_tile_key(f, &tiles) : 0;
     sfrt::TileSchedPtrs p;
+    cur_chain = scheds.pick(s);
+    sfrt::TileSched& sched = scheds.chain[cur_chain];
+    const ChainCam& chain_last = chain_cam[cur_chain];
     const long long cap0 = sched.cap;
     HIP_TRY(sched.begin(key, tiles, s, tile_order_on, p));
-    if (sched.cap != cap0) last_fill.valid = false;  // the cost buffers were reallocated
+    if (sched.cap != cap0 && last_fill.chain == cur_chain)
+      last_fill.valid = false;  // the cost buffers were reallocated
     f.tile_order = p.tile_order;
     f.tile_cost = p.tile_cost;
     f.prev_cost = p.prev_cost;
@@ -346,17 +351,18 @@ struct sfrt_world {
   int sched_end(const sfrt::FrameRec& f, hipStream_t s, bool queued) {
     sfrt::TileSchedPtrs p;
     p.tile_cost = f.tile_cost;
+    sfrt::TileSched& sched = scheds.chain[cur_chain];
     HIP_TRY(sched.end(p, s, queued));
     if (!queued) {
-      chain_last.valid = false;
-      last_fill.valid = false;
+      chain_cam[cur_chain].valid = false;
+      if (last_fill.chain == cur_chain) last_fill.valid = false;
       return SFRT_E_HIP;
     }
     if (sched.committed) {
-      chain_last = ChainCam{true, cam, f.sub_row0};
+      chain_cam[cur_chain] = ChainCam{true, cam, f.sub_row0};
       // that launch wrote its classes into cost[k % 2] before end() advanced k
       last_fill = LastFill{true, f.sub_row0, f.sub_rows, f.sub_w, sched.key_prev,
-                           (int)((sched.k - 1) & 1)};
+                           (int)((sched.k - 1) & 1), cur_chain};
     }
     return SFRT_OK;
   }
@@ -366,7 +372,8 @@ struct sfrt_world {
     bool valid = false;
     int row0 = 0, rows = 0, width = 0;
     long long key = 0;  // trace_tile_key: pixels per lane and the tile grid
-    int buf = 0;        // sched.cost[buf]
+    int buf = 0;        // scheds.chain[chain].cost[buf]
+    int chain = -1;
   };
   LastFill last_fill;
 
@@ -377,7 +384,7 @@ struct sfrt_world {
     sfrt_camera cam{};
     int sub_row0 = 0;
   };
-  ChainCam chain_last;
+  ChainCam chain_cam[sfrt::TileChains::kChains];  // per chain
 
   int read_status(hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
@@ -421,12 +428,13 @@ int sfrt_world_row_costs(sfrt_world* w, float* costs, int capacity, int* row0, i
   if (!L.valid) return SFRT_E_INVALID;
   const int tile_w = (int)((L.key >> 56) & 0x3f) * sfrt::kTile;
   const long long tiles_x = (L.key >> 28) & 0xfffffff, tiles_y = L.key & 0xfffffff;
-  if (tile_w <= 0 || tiles_x * tiles_y > w->sched.cap) return SFRT_E_INVALID;
+  const sfrt::TileSched& sched = w->scheds.chain[L.chain];
+  if (tile_w <= 0 || tiles_x * tiles_y > sched.cap) return SFRT_E_INVALID;
   if (capacity < L.rows) return SFRT_E_INVALID;
   sfrt::DeviceGuard g(w->device);
-  if (w->sched.have_last) HIP_TRY(hipStreamSynchronize(w->sched.last_stream));
+  if (sched.have_last) HIP_TRY(hipStreamSynchronize(sched.last_stream));
   std::vector<uint8_t> cls((size_t)(tiles_x * tiles_y));
-  HIP_TRY(hipMemcpy(cls.data(), w->sched.cost[L.buf], cls.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cls.data(), sched.cost[L.buf], cls.size(), hipMemcpyDeviceToHost));
   for (long long ty = 0; ty < tiles_y; ty++) {
     double c = 0.0;
     for (long long tx = 0; tx < tiles_x; tx++) {

@@ -104,3 +104,33 @@ def test_glsl_frames_in_flight(built, floor):
     for i in range(k):
         got = bufs[i].cpu().numpy().ravel()
         assert np.array_equal(got, want[i]), f"frame {i}: {_report(got, want[i], w)}"
+
+
+@pytest.mark.gpu
+def test_sphere_tile_order_chains_more_streams_than_chains(built, floor):
+    """The adaptive tile order keeps one chain per stream (sfrt_sched.h TileChains, 4
+    chains): frames round-robin over 6 streams in the ordered render_band path -- chains
+    taken over from other streams -- with the camera moving equal frames rendered alone."""
+    import sfrt
+    import torch
+    w, h, k = 1600, 1200, 18
+    sc = scenes.lcg64()
+    poses = [(0.01 * i, 0.0) for i in range(k)]
+    with sfrt.World(0) as world:
+        world.load_texture(*floor)
+        want = []
+        for p in poses:
+            world.set_scene(sc.posed(*p), w, h)
+            want.append(world.render())
+        bufs = [torch.empty(h, w * 4, dtype=torch.uint8, device="cuda") for _ in poses]
+        ss = _streams(6)
+        for rep in range(2):  # the second pass runs in orders built from the first
+            for i, p in enumerate(poses):
+                world.set_scene(sc.posed(*p), w, h)
+                world.render_band(bufs[i].data_ptr(), w * 4, 0, h, ss[(i + rep) % 6].cuda_stream)
+        torch.cuda.synchronize()
+        for s in ss:
+            world.check(s.cuda_stream)
+    for i in range(k):
+        got = bufs[i].cpu().numpy().ravel()
+        assert np.array_equal(got, want[i]), f"frame {i}: {_report(got, want[i], w)}"
