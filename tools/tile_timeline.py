@@ -1,6 +1,6 @@
 """Diagnostic: per-tile wall-clock start/end of the sphere kernel (a build with
 -DSFRT_EXP=16 writes them into pixels 0-3 of each tile's first row; wrong image bytes).
-    SFRT_LIB=sfml-software-raytracer_amd/build_x16/libsfrt.so python tools/tile_timeline.py
+    SFRT_LIB=sfml-software-raytracer_amd/build_x16/libsfrt.so python tools/tile_timeline.py [--1080]
 Prints the kernel's span, the distribution of tile durations, and when the longest
 tiles start and end, for a static and a turning camera."""
 import json
@@ -16,11 +16,12 @@ import sfrt  # noqa: E402
 
 
 def main():
-    W, H, R = 3840, 2160, 4
+    # --1080: the 1920x1080 10-sphere frame (16x8 tiles in the adaptive order)
+    W, H, R, sc = (1920, 1080, 2, scenes.default10()) if "--1080" in sys.argv else \
+        (3840, 2160, 4, scenes.lcg64())
     stream = torch.cuda.Stream()
     w = sfrt.World(0)
     w.load_texture(*scenes.load_floor())
-    sc = scenes.lcg64()
     out = {}
     for name, turn, order in (("static", False, 1), ("turning", True, 1), ("static_rowmajor", False, 0)):
         w.set_scene(sc, W, H)
