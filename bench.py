@@ -185,16 +185,25 @@ def frame_row_costs(world, rank, world_size, height, pitch, stream, device="cuda
     equal band once in the adaptive tile order, and the bands' costs are summed over ranks
     into one full-height vector (SURVEY 8e "Balance": cost-weighted band edges)."""
     r0, n = band_of(rank, world_size, height)
-    buf = torch.empty(max(n, 1), pitch, dtype=torch.uint8, device=device)
-    world.render_band(buf.data_ptr(), pitch, r0, n, stream.cuda_stream)
-    c0, cost = world.row_costs()
-    if (c0, cost.size) != (r0, n):
-        raise RuntimeError(f"row costs cover rows {c0}+{cost.size}, the band is {r0}+{n}")
-    full = torch.zeros(height, dtype=torch.float64, device=device)
-    full[c0:c0 + cost.size] = torch.from_numpy(cost.astype(np.float64)).to(device)
+    # the last element counts ranks whose costs failed: every rank still joins the
+    # all-reduce, and the tuner then falls back to row-weighted bands on every rank
+    full = torch.zeros(height + 1, dtype=torch.float64, device=device)
+    try:
+        buf = torch.empty(max(n, 1), pitch, dtype=torch.uint8, device=device)
+        world.render_band(buf.data_ptr(), pitch, r0, n, stream.cuda_stream)
+        c0, cost = world.row_costs()
+        if (c0, cost.size) != (r0, n):
+            raise RuntimeError(f"row costs cover rows {c0}+{cost.size}, the band is {r0}+{n}")
+        full[c0:c0 + cost.size] = torch.from_numpy(cost.astype(np.float64)).to(device)
+        del buf
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal to the run
+        print(f"rank {rank}: row costs unavailable ({e}); row-weighted bands only",
+              file=sys.stderr, flush=True)
+        full[height] = 1.0
     dist.all_reduce(full)
-    del buf
-    return full.cpu().numpy().astype(np.float32)
+    if float(full[height].item()) > 0:
+        return None
+    return full[:height].cpu().numpy().astype(np.float32)
 
 
 def tuned_pipeline(world, rank, world_size, height, pitch, stream):

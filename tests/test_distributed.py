@@ -147,6 +147,15 @@ def _row_cost_worker(rank, world_size, port, out_path):
                                  types.SimpleNamespace(cuda_stream=0), device="cpu")
     ok = [calls == [bands.band_of(rank, world_size, height)],
           bool(np.array_equal(cost, np.arange(1, height + 1, dtype=np.float32)))]
+
+    class BrokenOnRank1(FakeWorld):  # one rank's costs fail: every rank falls back
+        def row_costs(self):
+            if rank == 1:
+                raise RuntimeError("no ordered fill")
+            return super().row_costs()
+
+    ok.append(bench.frame_row_costs(BrokenOnRank1(), rank, world_size, height, pitch,
+                                    types.SimpleNamespace(cuda_stream=0), device="cpu") is None)
     spans = bands.cost_weighted_spans(cost, world_size, 1.0)
     got = torch.tensor([float(n) for _, n in spans], dtype=torch.float64)
     allv = [torch.zeros_like(got) for _ in range(world_size)]
