@@ -8,7 +8,7 @@
 // GL_NEAREST_MIPMAP_LINEAR sampling of the mipmapped REPEAT `ground`, unorm8
 // framebuffer rounding) and this kernel is held to the CPU restatement
 // (oracle/glsl_oracle.c) bit for bit.  Every expression keeps the shader's
-// operand order.  Sphere data are read at wave-uniform addresses; only the
+// operand order.  Sphere data are wave-uniform (scalar loads); only the
 // per-fragment lookups by drawSphere (:123-125, :154) are vector loads.
 #include <hip/hip_runtime.h>
 
@@ -51,8 +51,29 @@ __device__ __forceinline__ uint32_t unorm8(float v) {
   return (uint32_t)(int)floorf(v * 255.0f + 0.5f);
 }
 
-__device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __restrict__ walls,
-                                         const GlslBall* __restrict__ balls, int i, int row,
+// The wall / ball / pair tables through the constant address space (the kernel never
+// writes them): wave-uniform loads from it are scalar loads.
+template <typename T>
+using const_ptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ const_ptr<T> as_const(const T* p) {
+  return (const_ptr<T>)p;
+}
+template <typename T>
+__device__ __forceinline__ T ld(const_ptr<T> p, int i) {
+  static_assert(sizeof(T) % 4 == 0, "dword records");
+  const __attribute__((address_space(4))) uint32_t* q =
+      (const __attribute__((address_space(4))) uint32_t*)(p + i);
+  uint32_t w[sizeof(T) / 4];
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) w[k] = q[k];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
+}
+
+__device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall> walls,
+                                         const_ptr<GlslBall> balls, int i, int row,
                                          uint32_t& work, bool store = true) {
   const float fx = (float)i + 0.5f;
   const float fy = (float)(f.height - 1 - row) + 0.5f;
@@ -79,7 +100,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
   // point, so the remaining passes would repeat it and are skipped.
   bool moved = false;
   for (int j = f.wall_start, k = f.wall_start % (f.sc > 0 ? f.sc : 1); j < 3 * f.sc; j++) {
-    const GlslWall w = walls[k];
+    const GlslWall w = ld(walls, k);
     const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
     const float s = (rx * rx + ry * ry) + rz * rz;
     const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
@@ -131,7 +152,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
     // 0.5); it only changes when a ball's body runs.
     float thr = 1e30f;
     for (int k = 0; k < nballs; k++) {
-      const GlslBall b = balls[k];
+      const GlslBall b = ld(balls, k);
       const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
       const float ss = (ox * ox + oy * oy) + oz * oz;
       // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
@@ -200,7 +221,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
                        ((float)(f.sc + f.lc - 1) < (float)draw ? 0.0f : 1.0f);
   const int nshadow = f.all - f.sc - f.lc;
   for (int li = 0; li < f.lc; li++) {
-    const GlslBall L = balls[li];
+    const GlslBall L = ld(balls, li);
     const float tlx = L.x - px, tly = L.y - py, tlz = L.z - pz;
     const float tll = len3(tlx, tly, tlz);
     const float tnx = tlx / tll, tny = tly / tll, tnz = tlz / tll;
@@ -213,7 +234,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
       const float smooth_nm = t * t * (3.0f - 2.0f * t);                 // smoothstep(0, .5, nm)
       const bool near = total < 1000.0f;
       for (int k = 0; k < nshadow; k++) {
-        const GlslPair P = f.pairs[li * nshadow + k];
+        const GlslPair P = ld(as_const(f.pairs), li * nshadow + k);
         const float cosang = (-tnx * P.ux + -tny * P.uy) + -tnz * P.uz;
         // Ball outside the light cone seen from pos: acos(cosang) >= sanglet
         // (with margin) makes the clamp's argument >= 1, factor 1 exactly.
@@ -244,10 +265,9 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const GlslWall* __r
         unorm8(cr) | (unorm8(cg) << 8) | (unorm8(cbl) << 16) | (255u << 24);
 }
 
-// Wall and ball records are read once per visit by every wave at wave-uniform
-// addresses; staging them in LDS measured 5-10% slower (profiles/r1_glsl_variants.json),
-// scalar loads through the constant address space or a next-record prefetch 7-8%
-// slower (profiles/ab/r2_ab18).  Four 8x8 tiles (one per
+// Wall and ball records are read once per visit by every wave with scalar loads
+// (constant address space, above); staging them in LDS measured 5-10% slower
+// (profiles/r1_glsl_variants.json), a next-record prefetch 7-8% slower (profiles/ab/r2_ab18).  Four 8x8 tiles (one per
 // wave) per 256-thread workgroup, row-major.
 __global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
   const int lane = threadIdx.x & 63;
@@ -257,7 +277,7 @@ __global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
   const int r = ty * 8 + (lane >> 3);
   if (i >= f.width || r >= f.rows) return;
   uint32_t work = 0;
-  fragment(f, f.walls, f.balls, i, f.row0 + r, work);
+  fragment(f, as_const(f.walls), as_const(f.balls), i, f.row0 + r, work);
 }
 
 // One 8x8 tile per one-wave workgroup in the adaptive tile order (sfrt_device.h
@@ -285,7 +305,7 @@ __global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
   // branch around fragment() would cost its wave-uniform skips their uniformity.
   const bool in = i < f.width && r < f.rows;
   uint32_t work = 0;
-  fragment(f, f.walls, f.balls, i < f.width ? i : f.width - 1,
+  fragment(f, as_const(f.walls), as_const(f.balls), i < f.width ? i : f.width - 1,
                   f.row0 + (r < f.rows ? r : f.rows - 1), work, in);
   if (f.tile_cost) {
     const uint32_t w = wave_max_u32(work);  // the tile's longest march
