@@ -222,6 +222,22 @@ __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereR
   return __builtin_amdgcn_ballot_w64(inc);
 }
 
+// Record k read through the constant address space: the records are never written
+// while a launch runs (kernel arguments, or a device ring slot reused only after the
+// event of the launch that read it), and wave-uniform loads from that space are scalar
+// loads -- through the generic pointer the compiler must assume the frame's stores may
+// alias them and emits vector loads into VGPRs (the n > 64 kernel's records).
+__device__ __forceinline__ SphereRec rec_at(const SphereRec* p, int k) {
+  const __attribute__((address_space(4))) uint32_t* q =
+      (const __attribute__((address_space(4))) uint32_t*)(p + k);
+  uint32_t w[sizeof(SphereRec) / 4];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(SphereRec) / 4); i++) w[i] = q[i];
+  SphereRec r;
+  __builtin_memcpy(&r, w, sizeof r);
+  return r;
+}
+
 // std::max(largestDist, t) (SphereWorld.cpp:367) for L >= +0 and t > 0.01f
 // (the pass test), both finite: their bit patterns order like the values, so
 // one v_max_u32 gives the compare-select's bits (v_max_f32 would first
@@ -463,7 +479,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   // Every sphere in index order (no culling: cull off, or past kCullSafeIterations steps).
   auto visit_all = [&](float (&L)[R]) {
     for (int k = 0; k < f.n; k++) {
-      const SphereRec& s = sph[k];
+      const SphereRec s = rec_at(sph, k);
       visit(s.cx, s.cy, s.cz, s.r, s.s_pass, k, L);
     }
   };
@@ -489,8 +505,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       if (mm) {
         const int k = entry(__builtin_ctzll(mm));
         mm &= mm - 1;
-        scx[q] = sph[k].cx; scy[q] = sph[k].cy; scz[q] = sph[k].cz;
-        sr[q] = sph[k].r; ssp[q] = sph[k].s_pass;
+        const SphereRec s = rec_at(sph, k);
+        scx[q] = s.cx; scy[q] = s.cy; scz[q] = s.cz;
+        sr[q] = s.r; ssp[q] = s.s_pass;
         sk[q] = k;
       }
     }
@@ -537,11 +554,12 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
         uint64_t mm = win;
         int k = entry(__builtin_ctzll(mm));
         mm &= mm - 1;
-        float cx = sph[k].cx, cy = sph[k].cy, cz = sph[k].cz, rad = sph[k].r, sp = sph[k].s_pass;
+        const SphereRec s0 = rec_at(sph, k);
+        float cx = s0.cx, cy = s0.cy, cz = s0.cz, rad = s0.r, sp = s0.s_pass;
         for (;;) {
           const int kn = mm ? entry(__builtin_ctzll(mm)) : k;
-          const float ncx = sph[kn].cx, ncy = sph[kn].cy, ncz = sph[kn].cz, nr = sph[kn].r,
-                      nsp = sph[kn].s_pass;
+          const SphereRec sn = rec_at(sph, kn);
+          const float ncx = sn.cx, ncy = sn.cy, ncz = sn.cz, nr = sn.r, nsp = sn.s_pass;
           visit(cx, cy, cz, rad, sp, k, L);
           if (!mm) break;
           mm &= mm - 1;
@@ -619,8 +637,8 @@ __global__ __launch_bounds__(64, 8) void k_trace_window_r(InlineArgs args) {
   trace_tile_window_r<R, false>(args.f, args.s);
 }
 
-// n > 64: the records in device memory (f.spheres), the culled list per wave.  66
-// VGPRs at R = 4 (7 waves/SIMD; forcing 8 spilled two and gained nothing, ab/r2_ab12).
+// n > 64: the records in device memory (f.spheres, read with scalar loads: rec_at), the
+// culled list per wave.  57 VGPRs at R = 4 (8 waves/SIMD).
 template <int R>
 __global__ __launch_bounds__(64) void k_trace_window_list(FrameRec f) {
   trace_tile_window_r<R, true>(f, f.spheres);
