@@ -72,6 +72,19 @@ __device__ __forceinline__ float dv(float a, float b, float y) {
   return RECIP ? sfrt_math::div_recip(a, b, y) : a / b;
 }
 
+// Light j through the constant address space (the table is never written by a launch):
+// the wave-uniform loads become scalar loads instead of vector loads into VGPRs.
+__device__ __forceinline__ VoxLight light_at(const VoxLight* p, int j) {
+  const __attribute__((address_space(4))) uint32_t* q =
+      (const __attribute__((address_space(4))) uint32_t*)(p + j);
+  uint32_t w[sizeof(VoxLight) / 4];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(VoxLight) / 4); i++) w[i] = q[i];
+  VoxLight l;
+  __builtin_memcpy(&l, w, sizeof l);
+  return l;
+}
+
 __device__ __forceinline__ uint32_t pack(uint32_t r, uint32_t g, uint32_t b, uint32_t a) {
   return r | (g << 8) | (b << 16) | (a << 24);
 }
@@ -226,7 +239,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       float litr = l0 < 0.0f ? 0.0f : l0;
       float litg = litr, litb = litr;
       for (int j = 0; j < f.nlights; j++) {
-        const VoxLight& L = f.lights[j];
+        const VoxLight L = light_at(f.lights, j);
         const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
         float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
         float add = (L.intensity / dd - dd * 0.002f);
