@@ -207,18 +207,23 @@ def frame_row_costs(world, rank, world_size, height, pitch, stream, device="cuda
 
 
 def tuned_pipeline(world, rank, world_size, height, pitch, stream):
-    """Row bands for this node: tune_spans times root-weighted and cost-weighted partitions
-    with real frames (untimed warm-up) and keeps the fastest; N = 1 is one whole band."""
+    """Row bands for this node: tune_spans times root-weighted and cost-weighted partitions,
+    with RGBA8 and packed band transfers, on real frames (untimed warm-up) and keeps the
+    fastest; N = 1 is one whole band."""
     def render(band, row0, rows):
         world.render_band(band.data_ptr(), pitch, row0, rows, stream.cuda_stream)
     row_cost = frame_row_costs(world, rank, world_size, height, pitch, stream) \
         if world_size > 1 else None
+    # packed band transfers (3.125 B per pixel over the links) are a candidate when every
+    # texel's alpha is 0 or 255 (Floor.png's are; the same textures on every rank)
+    formats = (False, True) if world_size > 1 and world.alpha_binary() else (False,)
     spans, pick, table = tune_spans(render, rank, world_size, height, pitch, "cuda",
                                     sync=torch.cuda.synchronize, reduce_device="cuda",
-                                    row_cost=row_cost)
-    pipe = BandPipeline(rank, world_size, height, pitch, "cuda", spans=spans)
+                                    row_cost=row_cost, packed=formats)
+    pipe = BandPipeline(rank, world_size, height, pitch, "cuda", spans=spans,
+                        packed=pick["packed"])
     info = {"rows_per_rank": [n for _, n in spans], "root_factor": pick["root_factor"],
-            "weights": pick["weights"]}
+            "weights": pick["weights"], "transfer": "packed" if pick["packed"] else "rgba8"}
     if table:
         info["tuning_ms_per_frame"] = table
     return pipe, info

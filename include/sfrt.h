@@ -170,6 +170,27 @@ SFRT_API const char* sfrt_error_string(int code);
 SFRT_API int sfrt_version(void);
 
 /* ======================================================================
+ * Band transfer packing (the exchange step of SURVEY 8e).  A frame
+ * pixel's alpha is its texel's (SphereWorld.cpp:376-381, :109), and the
+ * reference's textures hold alpha 0 or 255 only, so a band whose alphas are all
+ * 0 or 255 packs losslessly into RGB plus one alpha bit: 3.125 bytes per pixel
+ * on the wire instead of 4.  Format: B = ceil(pixels / 256) blocks, B * 800
+ * bytes; [0, 768 B) pixel p's R, G, B at bytes 3p..3p+2 (zero past the last
+ * pixel), then [768 B, 800 B) the little-endian bit string whose bit p is set
+ * when pixel p's alpha is 255.  Asynchronous on `hip_stream` of the device
+ * current to the calling thread, which holds both buffers; dev_rgba 4-byte
+ * and dev_packed 8-byte aligned.  Pixels whose alpha is neither 0 nor 255
+ * unpack with alpha 0 -- pack only bands of a world whose
+ * sfrt_world_alpha_binary is 1.
+ * ====================================================================== */
+SFRT_API int64_t sfrt_band_packed_bytes(int64_t pixels);  /* < 0: invalid */
+SFRT_API int sfrt_band_pack(const void* dev_rgba, int64_t pixels, void* dev_packed, void* hip_stream);
+SFRT_API int sfrt_band_unpack(const void* dev_packed, int64_t pixels, void* dev_rgba, void* hip_stream);
+/* 1 when at least one texture is loaded and every texel of every loaded texture has
+ * alpha 0 or 255 (so every pixel the world renders does), else 0. */
+SFRT_API int sfrt_world_alpha_binary(const sfrt_world* w, int* binary);
+
+/* ======================================================================
  * One frame over several GPUs of this node (BASELINE configs 4-5):
  * the reference caller is ONE C++ process (Source.cpp:17-28,47-52) that fills
  * one sf::Image; here it fills it on n GPUs.  The frame is split into
@@ -204,6 +225,19 @@ SFRT_API int sfrt_multi_add_sphere(sfrt_multi* m, float x, float y, float z, flo
 SFRT_API int sfrt_multi_update_spheres(sfrt_multi* m);
 SFRT_API int sfrt_multi_set_sphere_textures(sfrt_multi* m, const int32_t* slots, int count);
 SFRT_API int sfrt_multi_set_option(sfrt_multi* m, int option, int value);
+/* Transfer format of the bands that cross a link (see "Band transfer packing"):
+ * SFRT_TRANSFER_AUTO (default) packs when every rank's world is alpha-binary
+ * (sfrt_world_alpha_binary), SFRT_TRANSFER_RGBA never packs, SFRT_TRANSFER_PACKED
+ * always does (sfrt_multi_render fails with SFRT_E_INVALID on a world that is not
+ * alpha-binary).  Packed bands travel by point-to-point transfers (RCCL) or peer
+ * copies and are unpacked into the frame on devices[0]; the frame's bytes are the
+ * same either way.  sfrt_multi_get_transfer: the setting and whether the last
+ * render packed. */
+#define SFRT_TRANSFER_AUTO 0
+#define SFRT_TRANSFER_RGBA 1
+#define SFRT_TRANSFER_PACKED 2
+SFRT_API int sfrt_multi_set_transfer(sfrt_multi* m, int format);
+SFRT_API int sfrt_multi_get_transfer(sfrt_multi* m, int* format, int* last_packed);
 /* Band heights: rows[r] for rank r (rank 0 first, sum = height at render time);
  * rows == NULL restores the default equal split (sfrt_multi_bands, factor 1). */
 SFRT_API int sfrt_multi_set_bands(sfrt_multi* m, const int* rows, int n);

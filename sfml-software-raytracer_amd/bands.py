@@ -19,7 +19,10 @@ Two things shape the partition on MI355X:
   split with one RCCL gather.
 
 ``BandPipeline`` double-buffers bands and frames so that the transfer of
-frame k overlaps the render of frame k + 1.
+frame k overlaps the render of frame k + 1.  With ``packed`` (bands of a world whose
+textures are alpha-binary, sfrt.World.alpha_binary) every band but rank 0's crosses
+the link in libsfrt's packed format (3.125 B per pixel instead of 4; include/sfrt.h
+"Band transfer packing") and rank 0 unpacks it into the frame on a stream of its own.
 """
 from __future__ import annotations
 
@@ -126,7 +129,7 @@ class BandPipeline:
     exchanged."""
 
     def __init__(self, rank: int, world_size: int, height: int, pitch: int, device,
-                 depth: int = 2, spans=None, local_depth: int = 1):
+                 depth: int = 2, spans=None, local_depth: int = 1, packed: bool = False):
         self.rank, self.world_size, self.height = rank, world_size, height
         self.spans = list(spans) if spans is not None else equal_spans(height, world_size)
         check_spans(self.spans, height)
@@ -154,6 +157,33 @@ class BandPipeline:
                 self.bands = [torch.empty(self.rows, pitch, dtype=torch.uint8, device=device)
                               for _ in range(self.depth)]
         self.pending = [[] for _ in range(self.depth)]
+        self.packed = bool(packed) and world_size > 1
+        if self.packed:
+            self._init_packed(pitch, device)
+
+    def _init_packed(self, pitch: int, device) -> None:
+        """Packed transfers: every non-root rank packs its band (sfrt_band_pack) into a
+        per-slot buffer and sends it point-to-point; rank 0 renders straight into its rows
+        of the frame, receives each band into a per-slot staging buffer and unpacks it into
+        the frame on `unpack_stream` (ordered after the receives, not after rank 0's
+        render of the next frame).  Needs a HIP device and pitch = width * 4."""
+        import sfrt
+        self._sfrt = sfrt
+        if pitch % 4:
+            raise ValueError("packed bands need whole RGBA8 rows")
+        self.pixels = [n * (pitch // 4) for _, n in self.spans]
+        nbytes = [sfrt.band_packed_bytes(p) for p in self.pixels]
+        if self.rank == 0:
+            self.bands = [v[0] for v in self.views]
+            self.stage = [[torch.empty(nbytes[r], dtype=torch.uint8, device=device)
+                           if r > 0 and self.pixels[r] else None for r in range(self.world_size)]
+                          for _ in range(self.depth)]
+            self.unpack_stream = torch.cuda.Stream(device=device)
+            self.unpacked = [torch.cuda.Event() for _ in range(self.depth)]
+            self.unpack_pending = [False] * self.depth
+        else:
+            self.packbuf = [torch.empty(max(nbytes[self.rank], 8), dtype=torch.uint8, device=device)
+                            for _ in range(self.depth)]
 
     def acquire(self, k: int):
         """The band buffer for frame k, once the transfer that last read it is done."""
@@ -161,6 +191,10 @@ class BandPipeline:
         for work in self.pending[b]:
             work.wait()
         self.pending[b] = []
+        if self.packed and self.rank == 0 and self.unpack_pending[b]:
+            # frame slot b and its staging buffers: free once the last unpacks are done
+            torch.cuda.current_stream().wait_event(self.unpacked[b])
+            self.unpack_pending[b] = False
         return self.bands[b]
 
     def submit(self, k: int) -> None:
@@ -170,6 +204,8 @@ class BandPipeline:
         b = k % self.depth
         band = self.bands[b]
         views = self.views[b] if self.rank == 0 else None
+        if self.packed:
+            return self._submit_packed(b, band, views)
         if self.equal:
             self.pending[b] = [dist.gather(band, views, dst=0, async_op=True)]
         elif self.rank == 0:
@@ -179,11 +215,36 @@ class BandPipeline:
         elif self.rows > 0:
             self.pending[b] = dist.batch_isend_irecv([dist.P2POp(dist.isend, band, 0)])
 
+    def _submit_packed(self, b: int, band, views) -> None:
+        sf = self._sfrt
+        if self.rank > 0:
+            if self.rows > 0:
+                sf.band_pack(band.data_ptr(), self.pixels[self.rank], self.packbuf[b].data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+                self.pending[b] = dist.batch_isend_irecv(
+                    [dist.P2POp(dist.isend, self.packbuf[b], 0)])
+            return
+        srcs = [r for r in range(1, self.world_size) if self.pixels[r]]
+        if not srcs:
+            return
+        works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.stage[b][r], r) for r in srcs])
+        with torch.cuda.stream(self.unpack_stream):
+            for work in works:
+                work.wait()  # the unpack stream waits for the receives
+            for r in srcs:
+                sf.band_unpack(self.stage[b][r].data_ptr(), self.pixels[r], views[r].data_ptr(),
+                               self.unpack_stream.cuda_stream)
+            self.unpacked[b].record(self.unpack_stream)
+        self.unpack_pending[b] = True
+
     def drain(self) -> None:
         for b in range(self.depth):
             for work in self.pending[b]:
                 work.wait()
             self.pending[b] = []
+            if self.packed and self.rank == 0 and self.unpack_pending[b]:
+                torch.cuda.current_stream().wait_event(self.unpacked[b])
+                self.unpack_pending[b] = False
 
     def frame(self, k: int):
         """Rank 0's assembled frame k (valid after drain() or the next acquire of its slot)."""
@@ -218,31 +279,35 @@ def run_frames(pipe: BandPipeline, render, frames: int, sync=lambda: None) -> fl
 
 def tune_spans(render, rank: int, world_size: int, height: int, pitch: int, device,
                factors=DEFAULT_FACTORS, frames: int = 8, warm: int = 2,
-               sync=lambda: None, reduce_device="cpu", row_cost=None):
+               sync=lambda: None, reduce_device="cpu", row_cost=None, packed=(False,)):
     """Pick the partition whose pipelined frames run fastest on this node.
 
     Candidates: root_weighted_spans for every factor and, given the frame's per-row work
     `row_cost` (sfrt_world_row_costs, the same on every rank), cost_weighted_spans for
-    every factor.  Every candidate runs `warm` + `frames` real frames through a
+    every factor, each with every transfer format in `packed` (False: RGBA8 bands, True:
+    packed bands).  Every candidate runs `warm` + `frames` real frames through a
     BandPipeline; the time that counts is the max over ranks (all-reduced, so every
     rank sees the same numbers and takes the same decision).  Returns (spans, pick,
-    {label: ms per frame}) with pick = {"root_factor": f, "weights": "rows" | "cost"}
-    and labels "f" / "cost:f"."""
+    {label: ms per frame}) with pick = {"root_factor": f, "weights": "rows" | "cost",
+    "packed": bool} and labels "f" / "cost:f", prefixed "packed:" for packed bands."""
     if world_size == 1:
-        return [(0, height)], {"root_factor": 1.0, "weights": "rows"}, {}
-    cands = [(f"{f}", {"root_factor": f, "weights": "rows"}, root_weighted_spans(height, world_size, f))
+        return [(0, height)], {"root_factor": 1.0, "weights": "rows", "packed": False}, {}
+    parts = [(f"{f}", {"root_factor": f, "weights": "rows"}, root_weighted_spans(height, world_size, f))
              for f in factors]
     if row_cost is not None:
-        cands += [(f"cost:{f}", {"root_factor": f, "weights": "cost"},
+        parts += [(f"cost:{f}", {"root_factor": f, "weights": "cost"},
                    cost_weighted_spans(row_cost, world_size, f)) for f in factors]
+    cands = [(("packed:" if pk else "") + label, dict(pick, packed=bool(pk)), spans)
+             for pk in packed for label, pick, spans in parts]
     table, best = {}, None
     tried = set()
     for label, pick, spans in cands:
-        key = tuple(spans)
+        key = (tuple(spans), pick["packed"])
         if key in tried:
             continue
         tried.add(key)
-        pipe = BandPipeline(rank, world_size, height, pitch, device, spans=spans)
+        pipe = BandPipeline(rank, world_size, height, pitch, device, spans=spans,
+                            packed=pick["packed"])
         run_frames(pipe, render, warm, sync)
         wall = max_over_ranks(run_frames(pipe, render, frames, sync), reduce_device)
         del pipe

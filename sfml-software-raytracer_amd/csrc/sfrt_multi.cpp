@@ -9,7 +9,9 @@
 // exchange step -- by RCCL (one ncclGather for equal bands, grouped
 // ncclSend/ncclRecv otherwise) or by peer copies over xGMI.  Per rank: a render
 // stream, a copy stream (RCCL's stream), two band buffers, so the transfer of
-// frame k overlaps the render of frame k + 1.
+// frame k overlaps the render of frame k + 1.  Bands of alpha-binary worlds cross
+// the link packed (band_pack.hip: 3.125 B per pixel instead of 4) and are unpacked
+// into the frame on devices[0].
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -130,6 +132,9 @@ struct Rank {
   hipStream_t render_s = nullptr, copy_s = nullptr;
   uint8_t* band[2] = {};
   size_t band_bytes = 0;
+  uint8_t* packed[2] = {};  // this rank's packed band (its device)
+  uint8_t* stage[2] = {};   // where it lands on devices[0]
+  size_t packed_bytes = 0;
   hipEvent_t rendered[2] = {}, copied[2] = {};
   bool copy_pending[2] = {};
   ncclComm_t comm = nullptr;
@@ -142,6 +147,10 @@ struct sfrt_multi {
   int transport = SFRT_MULTI_PEER;
   std::vector<int> rows_set;  // sfrt_multi_set_bands (empty: equal split)
   std::vector<int> last_rows; // the bands of the last render (sfrt_multi_row_costs)
+  int transfer = SFRT_TRANSFER_AUTO;
+  bool last_packed = false;   // the format of the last render's transfers
+  hipEvent_t unpacked[2] = {};  // devices[0]: the unpacks that read stage[slot]
+  bool unpack_pending[2] = {};
   int64_t k = 0;              // frames rendered (band buffer k % 2)
   hipEvent_t start = nullptr;  // on devices[0]: the caller's stream position at render
   hipStream_t out_s = nullptr;  // devices[0]: update_image's frame stream
@@ -161,6 +170,7 @@ struct sfrt_multi {
       sfrt::DeviceGuard g(r.device);
       for (int q = 0; q < 2; q++) {
         (void)hipFree(r.band[q]);
+        (void)hipFree(r.packed[q]);
         if (r.rendered[q]) (void)hipEventDestroy(r.rendered[q]);
         if (r.copied[q]) (void)hipEventDestroy(r.copied[q]);
       }
@@ -170,6 +180,10 @@ struct sfrt_multi {
     }
     if (!ranks.empty()) {
       sfrt::DeviceGuard g(ranks[0].device);
+      for (Rank& r : ranks)
+        for (int q = 0; q < 2; q++) (void)hipFree(r.stage[q]);
+      for (int q = 0; q < 2; q++)
+        if (unpacked[q]) (void)hipEventDestroy(unpacked[q]);
       if (out_s) {
         (void)hipStreamSynchronize(out_s);
         (void)hipStreamDestroy(out_s);
@@ -205,6 +219,41 @@ struct sfrt_multi {
     return at == height ? SFRT_OK : SFRT_E_INVALID;
   }
 
+  // Packed transfer buffers for bands of rows[r] x width pixels: rank r's packed[2] on
+  // its device, stage[2] on devices[0].  Growing them first drains every stream.
+  int packed_buffers(const std::vector<int>& rows, int width) {
+    for (size_t r = 1; r < ranks.size(); r++) {
+      Rank& R = ranks[r];
+      const int64_t b = sfrt_band_packed_bytes((int64_t)rows[r] * width);
+      if (b < 0) return SFRT_E_INVALID;
+      if ((size_t)b <= R.packed_bytes) continue;
+      for (Rank& Q : ranks) {
+        sfrt::DeviceGuard g(Q.device);
+        HIP_TRY(hipStreamSynchronize(Q.render_s));
+        HIP_TRY(hipStreamSynchronize(Q.copy_s));
+      }
+      {
+        sfrt::DeviceGuard g(R.device);
+        for (int q = 0; q < 2; q++) {
+          (void)hipFree(R.packed[q]);
+          R.packed[q] = nullptr;
+        }
+        R.packed_bytes = 0;
+        for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.packed[q], (size_t)b));
+      }
+      {
+        sfrt::DeviceGuard g(ranks[0].device);
+        for (int q = 0; q < 2; q++) {
+          (void)hipFree(R.stage[q]);
+          R.stage[q] = nullptr;
+        }
+        for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.stage[q], (size_t)b));
+      }
+      R.packed_bytes = (size_t)b;
+    }
+    return SFRT_OK;
+  }
+
   // Queue one frame: renders after `stream`'s queued work, complete at its next position.
   int render(uint8_t* frame, int64_t pitch, hipStream_t stream) {
     int width = 0, height = 0;
@@ -219,6 +268,19 @@ struct sfrt_multi {
     for (int r = 1; r < n; r++) equal = equal && rows[r] == rows[0];
     equal = equal && rows[0] > 0;
     const int slot = (int)(k & 1);
+    bool packed = false;
+    if (n > 1 && transfer != SFRT_TRANSFER_RGBA) {
+      bool binary = true;
+      for (Rank& R : ranks) {
+        int b = 0;
+        if ((rc = sfrt_world_alpha_binary(R.world, &b))) return rc;
+        binary = binary && b;
+      }
+      if (transfer == SFRT_TRANSFER_PACKED && !binary) return SFRT_E_INVALID;
+      packed = binary;
+    }
+    if (packed && (rc = packed_buffers(rows, width))) return rc;
+    last_packed = packed;
     {
       sfrt::DeviceGuard g(ranks[0].device);
       HIP_TRY(hipEventRecord(start, stream));
@@ -250,6 +312,9 @@ struct sfrt_multi {
       }
       if ((rc = sfrt_world_render_band(R.world, target, pitch, row0[r], rows[r], R.render_s)))
         return rc;
+      if (packed && r > 0 &&
+          (rc = sfrt_band_pack(target, (int64_t)rows[r] * width, R.packed[slot], R.render_s)))
+        return rc;
       HIP_TRY(hipEventRecord(R.rendered[slot], R.render_s));
       HIP_TRY(hipStreamWaitEvent(R.copy_s, R.rendered[slot], 0));
     }
@@ -262,7 +327,17 @@ struct sfrt_multi {
         if (rows[r] == 0) continue;
         const size_t count = (size_t)rows[r] * (size_t)pitch;
         uint8_t* send = r == 0 ? frame : R.band[slot];
-        if (equal) {  // in place on the root: its send buffer is frame + 0 * count
+        if (packed) {  // rank 0's rows are already in the frame
+          if (r > 0) {
+            const size_t bytes = (size_t)sfrt_band_packed_bytes((int64_t)rows[r] * width);
+            if (nc.send(R.packed[slot], bytes, ncclUint8, 0, R.comm, R.copy_s) != ncclSuccess ||
+                nc.recv(R.stage[slot], bytes, ncclUint8, r, ranks[0].comm, ranks[0].copy_s) !=
+                    ncclSuccess) {
+              (void)nc.group_end();
+              return SFRT_E_HIP;
+            }
+          }
+        } else if (equal) {  // in place on the root: its send buffer is frame + 0 * count
           if (nc.gather(send, r == 0 ? frame : send, count, ncclUint8, 0, R.comm, R.copy_s) !=
               ncclSuccess) {
             (void)nc.group_end();
@@ -278,6 +353,14 @@ struct sfrt_multi {
         }
       }
       NCCL_TRY(nc.group_end());
+      if (packed) {  // after the receives on the root's copy stream
+        sfrt::DeviceGuard g(ranks[0].device);
+        for (int r = 1; r < n; r++)
+          if (rows[r] > 0 &&
+              (rc = sfrt_band_unpack(ranks[r].stage[slot], (int64_t)rows[r] * width,
+                                     frame + (size_t)row0[r] * (size_t)pitch, ranks[0].copy_s)))
+            return rc;
+      }
       for (int r = 0; r < n; r++) {
         Rank& R = ranks[r];
         sfrt::DeviceGuard g(R.device);
@@ -292,16 +375,38 @@ struct sfrt_multi {
         Rank& R = ranks[r];
         if (rows[r] == 0) continue;
         sfrt::DeviceGuard g(R.device);
-        HIP_TRY(hipMemcpyPeerAsync(frame + (size_t)row0[r] * (size_t)pitch, ranks[0].device,
-                                   R.band[slot], R.device, (size_t)rows[r] * (size_t)pitch,
-                                   R.copy_s));
+        if (packed) {
+          // stage[slot] is free once the unpacks of two frames back have read it
+          if (unpack_pending[slot]) HIP_TRY(hipStreamWaitEvent(R.copy_s, unpacked[slot], 0));
+          HIP_TRY(hipMemcpyPeerAsync(R.stage[slot], ranks[0].device, R.packed[slot], R.device,
+                                     (size_t)sfrt_band_packed_bytes((int64_t)rows[r] * width),
+                                     R.copy_s));
+        } else {
+          HIP_TRY(hipMemcpyPeerAsync(frame + (size_t)row0[r] * (size_t)pitch, ranks[0].device,
+                                     R.band[slot], R.device, (size_t)rows[r] * (size_t)pitch,
+                                     R.copy_s));
+        }
         HIP_TRY(hipEventRecord(R.copied[slot], R.copy_s));
         R.copy_pending[slot] = true;
       }
       sfrt::DeviceGuard g(ranks[0].device);
       if (rows[0] > 0) HIP_TRY(hipStreamWaitEvent(stream, ranks[0].rendered[slot], 0));
-      for (int r = 1; r < n; r++)
-        if (rows[r] > 0) HIP_TRY(hipStreamWaitEvent(stream, ranks[r].copied[slot], 0));
+      if (packed) {  // unpack on the root's copy stream, after every band landed
+        hipStream_t us = ranks[0].copy_s;
+        for (int r = 1; r < n; r++)
+          if (rows[r] > 0) HIP_TRY(hipStreamWaitEvent(us, ranks[r].copied[slot], 0));
+        for (int r = 1; r < n; r++)
+          if (rows[r] > 0 &&
+              (rc = sfrt_band_unpack(ranks[r].stage[slot], (int64_t)rows[r] * width,
+                                     frame + (size_t)row0[r] * (size_t)pitch, us)))
+            return rc;
+        HIP_TRY(hipEventRecord(unpacked[slot], us));
+        unpack_pending[slot] = true;
+        HIP_TRY(hipStreamWaitEvent(stream, unpacked[slot], 0));
+      } else {
+        for (int r = 1; r < n; r++)
+          if (rows[r] > 0) HIP_TRY(hipStreamWaitEvent(stream, ranks[r].copied[slot], 0));
+      }
     }
     k++;
     return SFRT_OK;
@@ -359,6 +464,8 @@ int sfrt_multi_create(const int* hip_devices, int n, int transport, sfrt_multi**
   {
     sfrt::DeviceGuard g(hip_devices[0]);
     if (hipEventCreateWithFlags(&m->start, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->unpacked[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&m->unpacked[1], hipEventDisableTiming) != hipSuccess ||
         hipStreamCreateWithFlags(&m->out_s, hipStreamNonBlocking) != hipSuccess) {
       delete m;
       return SFRT_E_HIP;
@@ -437,6 +544,21 @@ int sfrt_multi_set_option(sfrt_multi* m, int option, int value) {
   if (!m) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(m->mu);
   return m->each([&](sfrt_world* w) { return sfrt_world_set_option(w, option, value); });
+}
+
+int sfrt_multi_set_transfer(sfrt_multi* m, int format) {
+  if (!m || format < SFRT_TRANSFER_AUTO || format > SFRT_TRANSFER_PACKED) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(m->mu);
+  m->transfer = format;
+  return SFRT_OK;
+}
+
+int sfrt_multi_get_transfer(sfrt_multi* m, int* format, int* last_packed) {
+  if (!m || !format || !last_packed) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(m->mu);
+  *format = m->transfer;
+  *last_packed = m->last_packed ? 1 : 0;
+  return SFRT_OK;
 }
 
 int sfrt_multi_set_bands(sfrt_multi* m, const int* rows, int n) {

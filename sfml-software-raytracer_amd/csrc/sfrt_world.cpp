@@ -120,6 +120,7 @@ struct sfrt_world {
   std::vector<uint8_t> tex_host[SFRT_TEXTURE_SLOTS];
   int tex_w[SFRT_TEXTURE_SLOTS] = {};
   int tex_h[SFRT_TEXTURE_SLOTS] = {};
+  bool tex_alpha01[SFRT_TEXTURE_SLOTS] = {};  // every texel's alpha is 0 or 255
   uint32_t tex_off[SFRT_TEXTURE_SLOTS] = {};  // texel offset of each slot in the atlas
   int cull = 1;
   int rays = 0;           // SFRT_OPT_RAYS_PER_LANE (0 = automatic)
@@ -515,6 +516,9 @@ int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int te
   w->tex_host[slot].assign(rgba, rgba + bytes);
   w->tex_w[slot] = tex_w;
   w->tex_h[slot] = tex_h;
+  bool a01 = true;
+  for (size_t i = 3; i < bytes && a01; i += 4) a01 = rgba[i] == 0 || rgba[i] == 255;
+  w->tex_alpha01[slot] = a01;
   // Rebuild the device atlas: textures[0] (SphereWorld.cpp:376-377) first, then
   // the extension slots.  Draws on any stream may still read the old atlas.
   size_t total = 0;
@@ -536,6 +540,19 @@ int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int te
     if (!w->tex_host[k].empty())
       HIP_TRY(hipMemcpy(w->d_tex + w->tex_off[k], w->tex_host[k].data(), w->tex_host[k].size(),
                         hipMemcpyHostToDevice));
+  return SFRT_OK;
+}
+
+int sfrt_world_alpha_binary(const sfrt_world* w, int* binary) {
+  if (!w || !binary) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(w->mu);
+  bool any = false, all = true;
+  for (int k = 0; k < SFRT_TEXTURE_SLOTS; k++) {
+    if (w->tex_host[k].empty()) continue;
+    any = true;
+    all = all && w->tex_alpha01[k];
+  }
+  *binary = any && all ? 1 : 0;
   return SFRT_OK;
 }
 

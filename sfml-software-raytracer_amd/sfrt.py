@@ -53,9 +53,12 @@ ABI_SYMBOLS = (
     "sfrt_multi_set_sphere_textures", "sfrt_multi_set_option", "sfrt_multi_set_bands",
     "sfrt_multi_bands", "sfrt_multi_render", "sfrt_multi_check", "sfrt_multi_update_image",
     "sfrt_world_row_costs", "sfrt_multi_cost_bands", "sfrt_multi_row_costs", "sfrt_multi_balance",
+    "sfrt_multi_set_transfer", "sfrt_multi_get_transfer", "sfrt_band_packed_bytes", "sfrt_band_pack",
+    "sfrt_band_unpack", "sfrt_world_alpha_binary",
 )
 
 SFRT_MULTI_AUTO, SFRT_MULTI_RCCL, SFRT_MULTI_PEER = 0, 1, 2
+SFRT_TRANSFER_AUTO, SFRT_TRANSFER_RGBA, SFRT_TRANSFER_PACKED = 0, 1, 2
 
 
 class SfrtError(RuntimeError):
@@ -179,6 +182,12 @@ def lib() -> ctypes.CDLL:
         "sfrt_multi_bands": ([c_int, c_int, c_float, vp, vp], c_int),
         "sfrt_multi_render": ([vp, vp, ctypes.c_int64, vp], c_int),
         "sfrt_multi_check": ([vp], c_int),
+        "sfrt_multi_set_transfer": ([vp, c_int], c_int),
+        "sfrt_multi_get_transfer": ([vp, P(c_int), P(c_int)], c_int),
+        "sfrt_band_packed_bytes": ([ctypes.c_int64], ctypes.c_int64),
+        "sfrt_band_pack": ([vp, ctypes.c_int64, vp, vp], c_int),
+        "sfrt_band_unpack": ([vp, ctypes.c_int64, vp, vp], c_int),
+        "sfrt_world_alpha_binary": ([W, P(c_int)], c_int),
         "sfrt_multi_update_image": ([vp, vp], c_int),
     }
     for name, (args, res) in sig.items():
@@ -388,6 +397,12 @@ class World:
                                           ctypes.byref(n)), "row_costs")
         return r0.value, out[:n.value].copy()
 
+    def alpha_binary(self) -> bool:
+        """sfrt_world_alpha_binary: every loaded texel's alpha is 0 or 255 (bands pack)."""
+        b = ctypes.c_int()
+        _check(lib().sfrt_world_alpha_binary(self._h, ctypes.byref(b)), "alpha_binary")
+        return bool(b.value)
+
     def trace_points(self, ij) -> list[dict]:
         ij = np.ascontiguousarray(np.asarray(ij, dtype=np.int32).reshape(-1, 2))
         out = (PixelDump * ij.shape[0])()
@@ -482,6 +497,26 @@ class VoxelWorld:
         _check(lib().sfrt_voxel_set_option(self._h, option, value), "voxel_set_option")
 
 
+def band_packed_bytes(pixels: int) -> int:
+    """sfrt_band_packed_bytes: bytes of a packed band of `pixels` pixels (3.125 B each)."""
+    b = lib().sfrt_band_packed_bytes(int(pixels))
+    if b < 0:
+        raise SfrtError(int(b), "band_packed_bytes")
+    return int(b)
+
+
+def band_pack(src_ptr: int, pixels: int, dst_ptr: int, stream: int = 0) -> None:
+    """sfrt_band_pack: RGBA8 device pixels -> the packed transfer format (asynchronous)."""
+    _check(lib().sfrt_band_pack(ctypes.c_void_p(src_ptr), int(pixels), ctypes.c_void_p(dst_ptr),
+                                ctypes.c_void_p(stream or None)), "band_pack")
+
+
+def band_unpack(src_ptr: int, pixels: int, dst_ptr: int, stream: int = 0) -> None:
+    """sfrt_band_unpack: the packed transfer format -> RGBA8 device pixels (asynchronous)."""
+    _check(lib().sfrt_band_unpack(ctypes.c_void_p(src_ptr), int(pixels), ctypes.c_void_p(dst_ptr),
+                                  ctypes.c_void_p(stream or None)), "band_unpack")
+
+
 def multi_bands(height: int, n: int, root_factor: float = 1.0) -> list[tuple[int, int]]:
     """sfrt_multi_bands: (row0, rows) per rank, rank 0 ~root_factor x the others' rows."""
     row0 = np.zeros(n, dtype=np.int32)
@@ -562,6 +597,17 @@ class Multi:
 
     def set_option(self, option: int, value: int) -> None:
         _check(lib().sfrt_multi_set_option(self._h, option, value), "multi_set_option")
+
+    def set_transfer(self, fmt: int) -> None:
+        """sfrt_multi_set_transfer: SFRT_TRANSFER_AUTO / _RGBA / _PACKED."""
+        _check(lib().sfrt_multi_set_transfer(self._h, int(fmt)), "multi_set_transfer")
+
+    def transfer(self) -> tuple[int, bool]:
+        """(the transfer setting, whether the last render packed its bands)."""
+        f, p = ctypes.c_int(), ctypes.c_int()
+        _check(lib().sfrt_multi_get_transfer(self._h, ctypes.byref(f), ctypes.byref(p)),
+               "multi_get_transfer")
+        return f.value, bool(p.value)
 
     def set_bands(self, rows=None) -> None:
         if rows is None:

@@ -300,3 +300,111 @@ def test_multi_row_costs_skip_empty_bands(floor_tex):
     w.close()
     assert r0 == 0
     np.testing.assert_array_equal(cost, want)
+
+
+class _LoopbackDist:
+    """In-process stand-in for torch.distributed's point-to-point calls, so that several
+    BandPipelines -- one per rank, all on cuda:0 -- run the packed-band path in one process
+    (RCCL refuses two ranks on one device, and gloo does not move device tensors).  Same
+    ordering contract as the NCCL backend: a transfer starts after the work queued on both
+    the sender's and the receiver's current streams when they posted it, runs on its own
+    stream, and Work.wait() makes the caller's current stream wait for it."""
+
+    isend, irecv = "isend", "irecv"
+
+    class P2POp:
+        def __init__(self, op, tensor, peer):
+            self.op, self.tensor, self.peer = op, tensor, peer
+
+    class Work:
+        done = None
+
+        def wait(self):
+            import torch
+            assert self.done is not None, "waited on an unmatched transfer"
+            torch.cuda.current_stream().wait_event(self.done)
+
+    def __init__(self):
+        import torch
+        self.current = 0
+        self.stream = torch.cuda.Stream()
+        self.posted = {}  # (src, dst, op) -> [(tensor, event, work)]
+
+    def is_initialized(self):
+        return True
+
+    def batch_isend_irecv(self, ops):
+        import torch
+        works = []
+        for op in ops:
+            w = self.Work()
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            send = op.op == self.isend
+            key = (self.current, op.peer) if send else (op.peer, self.current)
+            other = self.posted.get(key + (self.irecv if send else self.isend,), [])
+            if other:
+                t2, ev2, w2 = other.pop(0)
+                src, dst = (op.tensor, t2) if send else (t2, op.tensor)
+                assert src.numel() == dst.numel()
+                with torch.cuda.stream(self.stream):
+                    self.stream.wait_event(ev)
+                    self.stream.wait_event(ev2)
+                    dst.copy_(src)
+                    done = torch.cuda.Event()
+                    done.record(self.stream)
+                w.done = w2.done = done
+            else:
+                self.posted.setdefault(key + (op.op,), []).append((op.tensor, ev, w))
+            works.append(w)
+        return works
+
+
+@pytest.mark.parametrize("world_size,factor", [(3, 1.0), (4, 2.5)])
+def test_band_pipeline_packed_frames(floor_tex, monkeypatch, world_size, factor):
+    """bands.BandPipeline with packed transfers (bench.py's N > 1 path for alpha-binary
+    worlds): every non-root rank packs its band, rank 0 unpacks into the frame on its unpack
+    stream while the next frame renders.  Six frames, camera turning, queued back to back
+    (frame slots and staging buffers reused): the last two frames equal one-GPU frames."""
+    import torch
+
+    import bands
+    import sfrt
+    fake = _LoopbackDist()
+    monkeypatch.setattr(bands, "dist", fake)
+    width, height = 1000, 563
+    pitch = width * 4
+    sc = scenes.lcg64()
+    poses = [(0.3 * k, 0.05 * k - 0.1) for k in range(6)]
+    spans = bands.root_weighted_spans(height, world_size, factor)
+    stream = torch.cuda.Stream()
+    worlds, pipes = [], []
+    with torch.cuda.stream(stream):
+        for r in range(world_size):
+            w = sfrt.World(0)
+            w.load_texture(*floor_tex)
+            w.set_scene(sc, width, height)
+            assert w.alpha_binary()
+            worlds.append(w)
+            pipes.append(bands.BandPipeline(r, world_size, height, pitch, "cuda:0", spans=spans,
+                                            packed=True))
+        for k, p in enumerate(poses):
+            for r in list(range(1, world_size)) + [0]:  # the root posts its receives last
+                fake.current = r
+                worlds[r].set_camera(sc.cam_pos, *p)
+                band = pipes[r].acquire(k)
+                worlds[r].render_band(band.data_ptr(), pitch, pipes[r].row0, pipes[r].rows,
+                                      stream.cuda_stream)
+                pipes[r].submit(k)
+        for r in range(world_size):
+            fake.current = r
+            pipes[r].drain()
+    torch.cuda.synchronize()
+    for w in worlds:
+        w.check(stream.cuda_stream)
+    for k in (4, 5):
+        worlds[0].set_scene(sc.posed(*poses[k]), width, height)
+        want = worlds[0].render()
+        assert np.array_equal(pipes[0].frame(k).cpu().numpy().ravel(), want), k
+    for w in worlds:
+        w.close()
