@@ -229,6 +229,48 @@ def tuned_pipeline(world, rank, world_size, height, pitch, stream):
     return pipe, info
 
 
+def host_delivery(local_rank, floor, scene, width, height, frames, want):
+    """SURVEY 8d: the end-to-end rate with the frame copied into a host `sf::Uint8*` buffer
+    (PCIe included), reported beside the HBM-resident `value`, never as it.  "pipelined":
+    sfrt_world_submit_frame / wait_frame into two pinned frames (render k+1 overlaps the
+    copy of k); "sync": sfrt_world_update_image into a pageable buffer, one frame at a time.
+    Static camera, the headline scene; `want` is the device frame the host frames must equal."""
+    w = sfrt.World(local_rank)
+    w.load_texture(*floor)
+    w.set_scene(scene, width, height)
+    res = {}
+    bufs = [sfrt.HostFrame(width * height * 4) for _ in range(2)]
+    for n in (8, frames):  # warm-up, then timed
+        pending = []
+        t0 = time.perf_counter()
+        for k in range(n):
+            pending.append(w.submit_frame(bufs[k % 2]))
+            if len(pending) == 2:
+                w.wait_frame(pending.pop(0))
+        for t in pending:
+            w.wait_frame(t)
+        dt = time.perf_counter() - t0
+    same = all(np.array_equal(b.array, want) for b in bufs)
+    res["pipelined_pinned"] = {"Mrays_per_s": round(width * height * frames / dt / 1e6, 2),
+                               "fps": round(frames / dt, 2),
+                               "GB_per_s_to_host": round(width * height * 4 * frames / dt / 1e9, 2),
+                               "bit_identical_to_device_frame": same}
+    for b in bufs:
+        b.free()
+    out = np.zeros(width * height * 4, np.uint8)
+    for n in (4, max(4, frames // 4)):
+        t0 = time.perf_counter()
+        for _ in range(n):
+            w.update_image(out)
+        dt = time.perf_counter() - t0
+    res["sync_pageable"] = {"Mrays_per_s": round(width * height * n / dt / 1e6, 2),
+                            "fps": round(n / dt, 2),
+                            "GB_per_s_to_host": round(width * height * 4 * n / dt / 1e9, 2),
+                            "bit_identical_to_device_frame": bool(np.array_equal(out, want))}
+    w.close()
+    return res
+
+
 def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, stream):
     """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped transfer)."""
     world.set_scene(scene, width, height)
@@ -491,9 +533,12 @@ def main() -> None:
                 "frames_in_flight": 2, "streams": 2}
             w6.close()
             del pipe6
+        torch.cuda.synchronize()
+        gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()
+        result["also"]["3840x2160_lcg64_to_host"] = dict(
+            host_delivery(local_rank, floor, scene, WIDTH, height, 200, gpu_frame),
+            note="PCIe-inclusive (frame copied into a host buffer), not the HBM-resident value")
         if not args.no_cpu_baseline:
-            torch.cuda.synchronize()
-            gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()
             result["cpu_baseline"] = cpu_baseline(scene, WIDTH, height, floor, gpu_frame)
     if rank == 0:
         print(json.dumps(result), flush=True)
