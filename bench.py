@@ -288,8 +288,14 @@ def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, 
 
 
 # BASELINE.json configs 4 and 5 (and the 8K frame on one GPU): frame size by GPU count.
-EXTRA_FRAMES = {1: [(7680, 4320)], 2: [(7680, 4320)], 4: [(7680, 4320)],
-                8: [(7680, 4320), (16384, 16384)]}
+# The north star reports Mrays/s at 1080p / 4K / 8K at 1, 2, 4 and 8 GPUs: at N > 1 the
+# 1080p (full scene) and 4K frames are split over the ranks too (at N = 1 they are the
+# headline and the 1920x1080_default10 line).
+EXTRA_FRAMES = {1: [(7680, 4320, "lcg64")],
+                2: [(1920, 1080, "default10"), (3840, 2160, "lcg64"), (7680, 4320, "lcg64")],
+                4: [(1920, 1080, "default10"), (3840, 2160, "lcg64"), (7680, 4320, "lcg64")],
+                8: [(1920, 1080, "default10"), (3840, 2160, "lcg64"), (7680, 4320, "lcg64"),
+                    (16384, 16384, "lcg64")]}
 
 
 def host_cpu_info() -> dict:
@@ -453,8 +459,9 @@ def main() -> None:
     # its rows split over the ranks), measured after the main line.
     extra = {}
     if not (args.no_extra or args.headline_only):
-        for fw, fh in EXTRA_FRAMES.get(world_size, []):
-            extra[f"{fw}x{fh}_lcg64"] = measure_frame(w, scene, fw, fh, rank, world_size,
+        for fw, fh, sname in EXTRA_FRAMES.get(world_size, []):
+            sc_x = scene if sname == "lcg64" else scenes.SCENES[sname]()
+            extra[f"{fw}x{fh}_{sname}"] = measure_frame(w, sc_x, fw, fh, rank, world_size,
                                                       max(5, args.steps // 2), 2, stream)
         w.set_scene(scene, WIDTH, height)
     if rank == 0:
