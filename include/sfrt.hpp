@@ -228,6 +228,9 @@ class MultiSphereWorld {
   // Cost-weighted bands from the last frame's per-row march work (sfrt_multi_balance):
   // rank 0 (no link) gets root_factor shares of the work, every other GPU one share.
   void Balance(float root_factor = 1.0f) { check(sfrt_multi_balance(m_, root_factor), "balance"); }
+  // Band transfer format: SFRT_TRANSFER_AUTO (default: packed RGB + alpha bit when every
+  // texel's alpha is 0 or 255), SFRT_TRANSFER_RGBA or SFRT_TRANSFER_PACKED.
+  void SetTransfer(int format) { check(sfrt_multi_set_transfer(m_, format), "set_transfer"); }
   // The whole frame into a caller-owned sf::Uint8* RGBA8 buffer (width*height*4).
   void UpdateImage(uint8_t* pixels) {
     push_state();

@@ -141,19 +141,24 @@ int main(int argc, char** argv) {
       failures++;
     }
 
-    // ---- the same frame on several GPUs: devices {0, 0} (peer copies) and {0} (RCCL) ----
+    // ---- the same frame on several GPUs: devices {0, 0} (peer copies) and {0} (RCCL),
+    //      bands packed (the default for Floor.png's 0/255 alphas) and RGBA8 ----
     for (const std::vector<int>& devs : {std::vector<int>{0, 0}, std::vector<int>{0}}) {
-      sfrt::MultiSphereWorld multi(devs);
-      multi.LoadTexture(floor);
-      multi.SetSpheres(world.Spheres());
-      multi.width = world.width;
-      multi.height = world.height;
-      multi.cam = world.cam;
-      std::vector<uint8_t> mf(frame.size(), 0);
-      multi.UpdateImage(mf.data());
-      const std::string hm = fnv1a64(mf);
-      std::printf("multi x%zu 1920x1080 fnv1a64=%s want=%s\n", devs.size(), hm.c_str(), argv[2]);
-      if (hm != argv[2]) failures++;
+      for (int fmt : {SFRT_TRANSFER_AUTO, SFRT_TRANSFER_RGBA}) {
+        sfrt::MultiSphereWorld multi(devs);
+        multi.LoadTexture(floor);
+        multi.SetSpheres(world.Spheres());
+        multi.SetTransfer(fmt);
+        multi.width = world.width;
+        multi.height = world.height;
+        multi.cam = world.cam;
+        std::vector<uint8_t> mf(frame.size(), 0);
+        multi.UpdateImage(mf.data());
+        const std::string hm = fnv1a64(mf);
+        std::printf("multi x%zu transfer %d 1920x1080 fnv1a64=%s want=%s\n", devs.size(), fmt,
+                    hm.c_str(), argv[2]);
+        if (hm != argv[2]) failures++;
+      }
     }
 
     // ---- main(): shader uniforms and rt.draw (Source.cpp:143-153) at 320x180 ----
