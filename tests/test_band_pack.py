@@ -164,13 +164,14 @@ def test_rendered_frames_pack_losslessly(built):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", [1, 2])
-def test_multi_transfer_formats_same_frame(built, transport):
-    """sfrt_multi: RGBA and packed transfers give the same frame, equal and unequal bands;
-    AUTO packs an alpha-binary world and not one with a translucent texel; PACKED refuses it."""
+@pytest.mark.parametrize("transport,width", [(1, 1000), (2, 1000), (2, 1001)])
+def test_multi_transfer_formats_same_frame(built, transport, width):
+    """sfrt_multi: RGBA and packed transfers give the same frame, equal and unequal bands
+    (a 1001-pixel row makes band sizes that are not whole 4-pixel groups); AUTO packs an
+    alpha-binary world and not one with a translucent texel; PACKED refuses it."""
     import sfrt
     rgba, tw, th = scenes.load_floor()
-    width, height = 1000, 563
+    height = 563
     devs = [0] if transport == sfrt.SFRT_MULTI_RCCL else [0, 0, 0]
     sc = scenes.lcg64().posed(0.4, 0.1)
     with sfrt.World(0) as ref:
