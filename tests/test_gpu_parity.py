@@ -296,6 +296,21 @@ def test_errors_fail_loudly(world):
         world.set_spheres(np.array([[0, 0, 0, -1]], np.float32))
     with pytest.raises(sfrt.SfrtError):
         world.set_spheres(np.array([[0, 0, np.nan, 1]], np.float32))
+    too_many = scenes.lcg_spheres(count=1024, seed=5)  # 1025 with the centre sphere
+    assert too_many.shape[0] == 1025
+    with pytest.raises(sfrt.SfrtError) as e:
+        world.set_spheres(too_many)
+    assert e.value.code == -4  # SFRT_E_TOO_MANY (SFRT_MAX_SPHERES = 1024)
+
+
+def test_maximum_sphere_count_matches_oracle(world, floor):
+    """SFRT_MAX_SPHERES = 1024 spheres (16 culling-mask words): equal to the oracle."""
+    spheres = scenes.sort_spheres(scenes.lcg_spheres(count=1023, seed=99))
+    assert spheres.shape[0] == 1024
+    scene = scenes.Scene("lcg1024", spheres).posed(0.9, 0.1)
+    world.set_scene(scene, 320, 180)
+    want = oracle_for(scene, 320, 180, floor).render(host_threads())
+    assert diff_report(world.render(), want, 320) == ""
 
 
 @pytest.mark.parametrize("fn,arg", [("asinf", "1"), ("atanf", "1"), ("atan2f", "100000000"),
