@@ -229,6 +229,11 @@ def tuned_pipeline(world, rank, world_size, height, pitch, stream):
     return pipe, info
 
 
+def hbm_frac(rays: int, kernel_ms: float) -> float:
+    """The HBM roofline fraction of one launch: 4 algorithmic bytes per ray / kernel time."""
+    return round(BYTES_PER_RAY * rays / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 6) if kernel_ms > 0 else 0.0
+
+
 def host_delivery(local_rank, floor, scene, width, height, frames, want):
     """SURVEY 8d: the end-to-end rate with the frame copied into a host `sf::Uint8*` buffer
     (PCIe included), reported beside the HBM-resident `value`, never as it.  "pipelined":
@@ -475,7 +480,8 @@ def main() -> None:
         wall2, k2 = time_frames(w2, pipe2, 1920 * 4, args.steps, args.warmup, stream)
         result["also"]["1920x1080_default10"] = {
             "n_gpus": 1, "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
-            "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4)}
+            "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4),
+            "hbm_frac": hbm_frac(1920 * 1080, k2)}
         w2.close()
         # BASELINE config 3 with "all textures": every reference texture resident, one
         # per sphere (the per-sphere texture extension; the main line is textures[0]).
@@ -488,7 +494,8 @@ def main() -> None:
         wall3, k3 = time_frames(w3, pipe3, pitch, args.steps, args.warmup, stream)
         result["also"]["3840x2160_lcg64_all_textures"] = {
             "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall3 / 1e6, 2),
-            "fps": round(args.steps / wall3, 2), "kernel_ms": round(k3, 4)}
+            "fps": round(args.steps / wall3, 2), "kernel_ms": round(k3, 4),
+            "hbm_frac": hbm_frac(WIDTH * height, k3)}
         w3.close()
         del pipe3
         # The adaptive tile order dispatches each frame's tiles longest-first
@@ -509,6 +516,7 @@ def main() -> None:
             result["also"][key] = {
                 "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall4 / 1e6, 2),
                 "fps": round(args.steps / wall4, 2), "kernel_ms": round(k4, 4),
+                "hbm_frac": hbm_frac(WIDTH * height, k4),
                 "camera": "rotation = 0.004 rad x frame index" if moving else "static pose (0,0)",
                 "tile_order": "adaptive" if order else "row-major (SFRT_OPT_TILE_ORDER 0)"}
         w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
@@ -522,7 +530,8 @@ def main() -> None:
         wall5, k5 = time_frames(w5, pipe5, pitch, args.steps, args.warmup, stream)
         result["also"]["3840x2160_lcg256"] = {
             "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall5 / 1e6, 2),
-            "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4), "spheres": 256}
+            "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4), "spheres": 256,
+            "hbm_frac": hbm_frac(WIDTH * height, k5)}
         w5.close()
         del pipe5
         # Two frames in flight (see frame_streams): the 4K static and 1080p frames.
