@@ -22,7 +22,10 @@ constexpr int kMaxIterations = 1 << 20;  // march guard; the reference has none
 // goes further switches to the full sphere list for the rest of its march.
 constexpr int kCullSafeIterations = 1024;
 constexpr int kPairMinSpheres = 16;  // above this, n <= 64 frames use 16x8 tiles (2 px per lane)
-constexpr int kSlots = 2;  // culled spheres held in SGPRs per wave (measured best of 0-4, 6; tools/ab_libs.py)
+#ifndef SFRT_SLOTS
+#define SFRT_SLOTS 2
+#endif
+constexpr int kSlots = SFRT_SLOTS;  // culled spheres held in SGPRs per wave (2: best of 0-4, 6; profiles/ab/r2_ab32)
 
 // One sphere as the kernel reads it: 32 B, one s_load_dwordx8.
 struct SphereRec {
