@@ -1,7 +1,8 @@
 """Build-flag A/B of libsfrt.so builds, interleaved across processes, bytes checked.
 
     python tools/ab_libs.py --libs a.so,b.so,a.so@3 [--rounds 3] [--reps 40] [--cases 4k,4k_rot,...]
-(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE; lib#K sets SFRT_SPLIT=K)
+(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE; lib#K sets SFRT_AB_KNOB=K for an
+experimental build that reads it -- r2_ab28 read it as SFRT_SPLIT; the product reads none)
 
 Each round starts one process per library (SFRT_LIB=<lib>, the same sfrt.py), which
 times every case with HIP events (median kernel time, event-pair overhead subtracted;
@@ -92,11 +93,11 @@ def main():
     for rnd in range(a.rounds):
         for lib in libs:  # "path" or "path@R" (R = SFRT_OPT_RAYS_PER_LANE); "path!" = timing probe
             probe = lib.endswith("!")
-            spec, _, split = lib.rstrip("!").partition("#")  # "#K": SFRT_SPLIT=K (longest tiles halved)
+            spec, _, knob = lib.rstrip("!").partition("#")  # "#K": SFRT_AB_KNOB=K for an A/B build
             path, _, rays = spec.partition("@")
             env = dict(os.environ, SFRT_LIB=os.path.abspath(path))
-            if split:
-                env["SFRT_SPLIT"] = split
+            if knob:
+                env["SFRT_AB_KNOB"] = knob
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
                                 "--cases", a.cases, "--reps", str(a.reps), "--rays", rays or "0"],
                                capture_output=True, text=True, env=env, timeout=600)
