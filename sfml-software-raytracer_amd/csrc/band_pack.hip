@@ -57,14 +57,21 @@ __global__ __launch_bounds__(kThreads) void k_band_pack(const uint32_t* __restri
   if (l16 == 0) bits[t >> 4] = word;
 }
 
-__global__ __launch_bounds__(kThreads) void k_band_unpack(const uint32_t* __restrict__ rgb,
+struct Rgb4 {  // one lane's 12 bytes of RGB (one dwordx3 load)
+  uint32_t w0, w1, w2;
+};
+
+// A16: the RGBA destination is 16-byte aligned, so a lane's 4 pixels are one dwordx4 store.
+template <bool A16>
+__global__ __launch_bounds__(kThreads) void k_band_unpack(const Rgb4* __restrict__ rgb,
                                                           const uint64_t* __restrict__ bits,
                                                           int64_t pixels,
                                                           uint32_t* __restrict__ rgba) {
   const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int64_t p0 = t * 4;
   if (p0 >= pixels) return;
-  const uint32_t w0 = rgb[3 * t + 0], w1 = rgb[3 * t + 1], w2 = rgb[3 * t + 2];
+  const Rgb4 v = rgb[t];
+  const uint32_t w0 = v.w0, w1 = v.w1, w2 = v.w2;
   const uint32_t nib = (uint32_t)(bits[t >> 4] >> (4 * (int)(t & 15)));
   const uint32_t a = 0xff000000u;
   uint32_t px[4];
@@ -72,7 +79,11 @@ __global__ __launch_bounds__(kThreads) void k_band_unpack(const uint32_t* __rest
   px[1] = (w0 >> 24) | ((w1 & 0xffffu) << 8) | ((nib & 2u) ? a : 0u);
   px[2] = (w1 >> 16) | ((w2 & 0xffu) << 16) | ((nib & 4u) ? a : 0u);
   px[3] = (w2 >> 8) | ((nib & 8u) ? a : 0u);
-  if (p0 + 3 < pixels) {
+  if (A16 && p0 + 3 < pixels) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 q = {px[0], px[1], px[2], px[3]};
+    __builtin_nontemporal_store(q, (u32x4*)(rgba + p0));
+  } else if (p0 + 3 < pixels) {
 #pragma unroll
     for (int i = 0; i < 4; i++) __builtin_nontemporal_store(px[i], rgba + p0 + i);
   } else {
@@ -118,11 +129,15 @@ int sfrt_band_unpack(const void* dev_packed, int64_t pixels, void* dev_rgba, voi
   if (!args_ok(dev_rgba, pixels, dev_packed)) return SFRT_E_INVALID;
   if (pixels == 0) return SFRT_OK;
   const int64_t blocks = blocks_of(pixels);
-  const uint32_t* rgb = (const uint32_t*)dev_packed;
+  const Rgb4* rgb = (const Rgb4*)dev_packed;
   const uint64_t* bits = (const uint64_t*)((const uint8_t*)dev_packed + blocks * kBlockRgb);
   const int64_t grid = (blocks * 64 + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(k_band_unpack, dim3((unsigned)grid), dim3(kThreads), 0,
-                     (hipStream_t)hip_stream, rgb, bits, pixels, (uint32_t*)dev_rgba);
+  if (((uintptr_t)dev_rgba & 15u) == 0)
+    hipLaunchKernelGGL(k_band_unpack<true>, dim3((unsigned)grid), dim3(kThreads), 0,
+                       (hipStream_t)hip_stream, rgb, bits, pixels, (uint32_t*)dev_rgba);
+  else
+    hipLaunchKernelGGL(k_band_unpack<false>, dim3((unsigned)grid), dim3(kThreads), 0,
+                       (hipStream_t)hip_stream, rgb, bits, pixels, (uint32_t*)dev_rgba);
   HIP_TRY(hipGetLastError());
   return SFRT_OK;
 }
