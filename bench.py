@@ -376,6 +376,9 @@ def main() -> None:
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    if sfrt.build_flavour() != "release":
+        raise SystemExit(f"bench.py measures the release library only; {sfrt.LIB_PATH} reports "
+                         f"build flavour {sfrt.build_flavour()!r} (unset SFRT_LIB, rebuild)")
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -140,7 +140,12 @@ SFRT_API int sfrt_world_wait_frame(sfrt_world* w, int64_t ticket);
 SFRT_API int sfrt_host_alloc(void** ptr, int64_t bytes);
 SFRT_API int sfrt_host_free(void* ptr);
 
-/* Float intermediates for `count` pixels (ij = i0, j0, i1, j1, ...), synchronous. */
+/* Float intermediates for `count` pixels (ij = i0, j0, i1, j1, ...), synchronous: the
+ * march position, drawSphere and loop trips of SphereWorld.cpp:362-372, xcoord, ycoord,
+ * brightness and the texel of :373-377, and the RGBA8 pixel, read out of the frame-fill
+ * kernel itself (its DUMP instantiation renders the whole frame with the world's options:
+ * tile shape, culling, and -- SFRT_OPT_TILE_ORDER on -- three launches in the adaptive
+ * order).  A pixel may be listed more than once. */
 SFRT_API int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pixel_dump* out);
 
 /* Options: SFRT_OPT_CULL (1 = per-wave sphere culling, default; 0 = visit
@@ -168,16 +173,21 @@ SFRT_API float sfrt_deg_to_rad(float deg);
 SFRT_API float sfrt_pass_threshold(float radius);
 SFRT_API const char* sfrt_error_string(int code);
 SFRT_API int sfrt_version(void);
+/* "release" for the shipped build; "diagnostic" for a -DSFRT_EXP timing/counter build
+ * (writes wrong bytes by design) and "ab" for a build with extra flags (build-flag A/B).
+ * bench.py refuses anything but "release". */
+SFRT_API const char* sfrt_build_flavour(void);
 
 /* ======================================================================
  * Band transfer packing (the exchange step of SURVEY 8e).  A frame
  * pixel's alpha is its texel's (SphereWorld.cpp:376-381, :109), and the
  * reference's textures hold alpha 0 or 255 only, so a band whose alphas are all
  * 0 or 255 packs losslessly into RGB plus one alpha bit: 3.125 bytes per pixel
- * on the wire instead of 4.  Format: B = ceil(pixels / 256) blocks, B * 800
- * bytes; [0, 768 B) pixel p's R, G, B at bytes 3p..3p+2 (zero past the last
- * pixel), then [768 B, 800 B) the little-endian bit string whose bit p is set
- * when pixel p's alpha is 255.  Asynchronous on `hip_stream` of the device
+ * on the wire instead of 4.  Format: B = ceil(pixels / 256), B * 800 bytes in two
+ * planes: [0, 768*B) the RGB plane, pixel p's R, G, B at bytes 3p..3p+2 (zero past
+ * the last pixel), then [768*B, 800*B) the alpha plane, the little-endian bit string
+ * whose bit p is set when pixel p's alpha is 255 (zero past the last pixel).
+ * Asynchronous on `hip_stream` of the device
  * current to the calling thread, which holds both buffers; dev_rgba 4-byte
  * and dev_packed 8-byte aligned.  Pixels whose alpha is neither 0 nor 255
  * unpack with alpha 0 -- pack only bands of a world whose

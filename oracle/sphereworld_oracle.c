@@ -23,12 +23,16 @@
  * (glibc 2.35 here and on the GPU box: sinf, cosf, atan2f, asinf), exactly
  * what the reference calls through std::sin / std::atan2 / std::asinf.
  *
- * Pinning: the reference itself cannot be built in this image (it needs
- * SFML 2.4.2, which is absent, and stand-in headers are not allowed), and it
- * ships no tests or golden data.  This restatement is pinned against the
- * FNV-1a-64 frame hashes that the survey recorded from the unmodified
- * reference TU (SURVEY.md section 6 / BASELINE.md); tests/test_oracle_golden.py
- * reproduces every one of them.  See DESIGN.md "Parity pinning".
+ * PARITY UNPINNED.  The reference itself cannot be built in this image: it
+ * needs SFML 2.4.2 (SphereWorld.h:3 includes <SFML/Graphics.hpp>), which is
+ * absent, and stand-in headers are not allowed.  It ships no tests, fixtures or
+ * golden data.  So nothing here pins this restatement to the reference's own
+ * output.  What exists is a sanity check: the survey's per-pixel march
+ * iteration statistics from a stub-SFML build, which
+ * tests/test_oracle_golden.py reproduces.  The survey's FNV-1a-64 frame hashes
+ * from that stub build do NOT reproduce (the stub's Image/Color semantics are
+ * unrecorded).  tests/golden/ holds hashes generated from THIS file.  See
+ * DESIGN.md section 3.
  */
 #include <math.h>
 #include <pthread.h>

@@ -8,11 +8,12 @@
 // the loaded ones).  Such a band packs losslessly into 3 bytes of RGB plus one
 // alpha bit per pixel: 3.125 B instead of 4 (22% fewer bytes over the link).
 //
-// Layout for P pixels, B = ceil(P / 256) blocks, B * 800 bytes:
-//   [0, 768 B)      RGB, pixel p at bytes 3p .. 3p+2 (R, G, B); bytes past pixel P
-//                   in the last block are zero;
-//   [768 B, 800 B)  alpha bits, bit p of the little-endian bit string = pixel p's
-//                   alpha is 255 (0 = alpha 0); bits past P are zero.
+// Layout for P pixels, B = ceil(P / 256) blocks, B * 800 bytes in two planes (the
+// RGB of every block first, then every block's alpha bits):
+//   [0, 768 B * B)            RGB plane, pixel p at bytes 3p .. 3p+2 (R, G, B);
+//                             bytes past pixel P in the last block are zero;
+//   [768 B * B, 800 B * B)    alpha plane, bit p of the little-endian bit string =
+//                             pixel p's alpha is 255 (0 = alpha 0); bits past P are zero.
 // Both kernels are HBM-streaming: a lane moves 4 pixels (16 B in, 12 B + 4 bits
 // out, or back), a wave one 256-pixel block.
 #include <hip/hip_runtime.h>

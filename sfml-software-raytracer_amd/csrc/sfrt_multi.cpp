@@ -604,6 +604,7 @@ int sfrt_multi_row_costs(sfrt_multi* m, float* costs, int height) {
     if (h != height) return SFRT_E_INVALID;
     std::vector<float> c((size_t)height);
     if ((rc = sfrt_world_row_costs(R.world, c.data(), height, &r0, &nr))) return rc;
+    if (r0 < 0 || nr < 0 || (int64_t)r0 + nr > height) return SFRT_E_INVALID;
     for (int j = 0; j < nr; j++) {
       costs[r0 + j] = c[(size_t)j];
       seen[(size_t)(r0 + j)] = 1;

@@ -91,8 +91,8 @@ struct TileSched {
   // false: it failed).  A failed launch restarts the chain: its cost buffer was
   // never written, so no later launch may sort it or read an order built from it.
   hipError_t end(const TileSchedPtrs& p, hipStream_t s, bool queued = true) {
+    committed = false;  // also for a launch outside the chain (no stale "committed")
     if (!p.tile_cost) return hipSuccess;
-    committed = false;
     if (!queued) {
       reset();
       return hipSuccess;

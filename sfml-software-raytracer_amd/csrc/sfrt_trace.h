@@ -82,18 +82,28 @@ struct InlineArgs {
 struct PixelDump {
   float pos[3];
   int draw;
-  int iters;
+  int iters;  // loop trips of SphereWorld.cpp:362 (the host's first one included)
   float xcoord, ycoord, brightness;
   uint32_t texel[2];
   uint32_t rgba;
 };
 
-// sphere_trace.hip
-int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream);
+// Float intermediates out of the frame-fill kernels themselves (sfrt_world_trace_points):
+// the DUMP instantiation of the same march and shading, plus an epilogue that writes
+// pixel (a, b)'s record to out[index[(b - sub_row0) * sub_w + a]] when that is >= 0.
+struct DumpArgs {
+  const int32_t* index;  // sub_rows x sub_w, -1 = no record
+  PixelDump* out;
+};
+
+// sphere_trace.hip.  dump != nullptr: the DUMP instantiation of the kernel the table picks.
+int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream,
+                 const DumpArgs* dump = nullptr);
+// "release" for the shipped build; "diagnostic" (-DSFRT_EXP: wrong bytes by design) or
+// "ab" (EXTRA build flags, tools/ab_libs.py) otherwise.
+const char* trace_build_flavour();
 // Tile grid of the kernel launch_trace picks for f when that kernel takes part in
 // the adaptive tile order: a key naming the grid (> 0) and its tile count; else 0.
 long long trace_tile_key(const FrameRec& f, long long* tiles);
-int launch_trace_points(const FrameRec& f, const int* dev_ij, int count, PixelDump* dev_out,
-                        void* stream);
 
 }  // namespace sfrt

@@ -364,6 +364,8 @@ struct sfrt_world {
       // that launch wrote its classes into cost[k % 2] before end() advanced k
       last_fill = LastFill{true, f.sub_row0, f.sub_rows, f.sub_w, sched.key_prev,
                            (int)((sched.k - 1) & 1), cur_chain};
+    } else {
+      last_fill.valid = false;  // this fill recorded no classes (tile order off, probe)
     }
     return SFRT_OK;
   }
@@ -478,6 +480,11 @@ void sfrt_world_destroy(sfrt_world* w) { delete w; }
 int sfrt_world_set_size(sfrt_world* w, int width, int height) {
   if (!w || width <= 0 || height <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(w->mu);
+  if (width != w->width || height != w->height) {
+    // the last fill's rows and tile grid belong to the old frame (sfrt_world_row_costs)
+    w->last_fill.valid = false;
+    for (auto& c : w->chain_cam) c.valid = false;
+  }
   w->width = width;
   w->height = height;
   return SFRT_OK;
@@ -753,31 +760,72 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
       return SFRT_E_INVALID;
   if (count == 0) return SFRT_OK;
   static_assert(sizeof(sfrt_pixel_dump) == sizeof(sfrt::PixelDump), "dump layout");
+  // The listed pixels come out of the frame-fill kernel itself (its DUMP instantiation,
+  // sphere_trace.hip): a whole frame with the world's options -- the kernel table's tile
+  // shape or SFRT_OPT_RAYS_PER_LANE, culling -- in the adaptive tile order when that is
+  // on (three launches on the world's stream, so the last one runs in a sorted order),
+  // row-major otherwise.  index: pixel -> first listed position (repeats copied below).
+  const size_t px = (size_t)w->width * w->height;
+  std::vector<int32_t> index(px, -1);
+  for (int k = 0; k < count; k++) {
+    int32_t& q = index[(size_t)ij[2 * k + 1] * w->width + ij[2 * k]];
+    if (q < 0) q = k;
+  }
   sfrt::DeviceGuard g(w->device);
-  sfrt::FrameRec f;
-  std::vector<sfrt::SphereRec> recs;
-  w->prepare(f, recs);
-  rc = w->stage_spheres(f, recs, w->stream, true);
-  if (rc) return rc;
-  int32_t* d_ij = nullptr;
-  sfrt::PixelDump* d_out = nullptr;
-  if (hipMalloc(&d_ij, sizeof(int32_t) * 2 * (size_t)count) != hipSuccess ||
-      hipMalloc(&d_out, sizeof(sfrt::PixelDump) * (size_t)count) != hipSuccess) {
-    (void)hipFree(d_ij);
+  if (w->d_frame_px < px) {
+    (void)hipFree(w->d_frame);
+    w->d_frame = nullptr;
+    w->d_frame_px = 0;
+    HIP_TRY(hipMalloc(&w->d_frame, px * 4));
+    w->d_frame_px = px;
+  }
+  sfrt::DumpArgs dump{};
+  if (hipMalloc((void**)&dump.index, sizeof(int32_t) * px) != hipSuccess ||
+      hipMalloc(&dump.out, sizeof(sfrt::PixelDump) * (size_t)count) != hipSuccess) {
+    (void)hipFree((void*)dump.index);
     return SFRT_E_HIP;
   }
-  rc = SFRT_OK;
-  if (hipMemcpyAsync(d_ij, ij, sizeof(int32_t) * 2 * (size_t)count, hipMemcpyHostToDevice,
-                     w->stream) != hipSuccess ||
-      sfrt::launch_trace_points(f, d_ij, count, d_out, w->stream) ||
-      w->launched(w->stream) != SFRT_OK ||
-      hipMemcpyAsync(out, d_out, sizeof(sfrt::PixelDump) * (size_t)count, hipMemcpyDeviceToHost,
-                     w->stream) != hipSuccess)
-    rc = SFRT_E_HIP;
+  auto run = [&]() -> int {
+    HIP_TRY(hipMemcpyAsync((void*)dump.index, index.data(), sizeof(int32_t) * px,
+                           hipMemcpyHostToDevice, w->stream));
+    const int passes = w->tile_order_on ? 3 : 1;
+    for (int q = 0; q < passes; q++) {
+      sfrt::FrameRec f;
+      std::vector<sfrt::SphereRec> recs;
+      w->prepare(f, recs);
+      f.xstart = 0; f.xadd = 1; f.ystart = 0; f.yadd = 1;
+      f.sub_w = w->width;
+      f.sub_row0 = 0;
+      f.sub_rows = w->height;
+      f.tiles_x = (w->width + sfrt::kTile - 1) / sfrt::kTile;
+      f.out = w->d_frame;
+      f.out_pitch = w->width;
+      int rc2 = w->stage_spheres(f, recs, w->stream, false);
+      if (rc2) return rc2;
+      if (w->tile_order_on) {
+        if ((rc2 = w->sched_begin(f, w->stream))) return rc2;
+        if ((rc2 = w->sched_end(f, w->stream,
+                                sfrt::launch_trace(f, recs.data(), w->stream, &dump) == 0)))
+          return rc2;
+      } else if (sfrt::launch_trace(f, recs.data(), w->stream, &dump)) {
+        return SFRT_E_HIP;
+      }
+      if ((rc2 = w->launched(w->stream))) return rc2;
+    }
+    HIP_TRY(hipMemcpyAsync(out, dump.out, sizeof(sfrt::PixelDump) * (size_t)count,
+                           hipMemcpyDeviceToHost, w->stream));
+    return SFRT_OK;
+  };
+  rc = run();
   const int st = w->read_status(w->stream);
-  (void)hipFree(d_ij);
-  (void)hipFree(d_out);
-  return rc ? rc : st;
+  (void)hipFree((void*)dump.index);
+  (void)hipFree(dump.out);
+  if (rc || st) return rc ? rc : st;
+  for (int k = 0; k < count; k++) {
+    const int32_t q = index[(size_t)ij[2 * k + 1] * w->width + ij[2 * k]];
+    if (q != k) out[k] = out[q];
+  }
+  return SFRT_OK;
 }
 
 int sfrt_host_alloc(void** ptr, int64_t bytes) {
@@ -895,6 +943,8 @@ const char* sfrt_error_string(int code) {
   }
 }
 
-int sfrt_version(void) { return 1; }
+int sfrt_version(void) { return 3; }
+
+const char* sfrt_build_flavour(void) { return sfrt::trace_build_flavour(); }
 
 }  // extern "C"

@@ -35,6 +35,9 @@
 #ifndef SFRT_EXP
 #define SFRT_EXP 0
 #endif
+#ifndef SFRT_BUILD_FLAVOUR
+#define SFRT_BUILD_FLAVOUR "release"
+#endif
 
 namespace sfrt {
 namespace {
@@ -129,16 +132,6 @@ __device__ __forceinline__ uint32_t shade_rgba(uint32_t texel, float brightness)
   const uint32_t g = __float2uint_rz((float)((texel >> 8) & 0xffu) * brightness);
   const uint32_t b = __float2uint_rz((float)((texel >> 16) & 0xffu) * brightness);
   return (r & 0xffu) | ((g & 0xffu) << 8) | ((b & 0xffu) << 16) | (texel & 0xff000000u);
-}
-
-// Both parts for one pixel (the parity kernel k_trace_points).
-__device__ __forceinline__ uint32_t shade(const FrameRec& f, const SphereRec& d, float px,
-                                         float py, float pz, PixelDump* dump) {
-  const Shading sh = shade_texel(f, d, px, py, pz, dump);
-  if (sh.outside) atomicOr(f.status, 2);
-  const uint32_t rgba = shade_rgba(sh.outside ? 0u : f.tex[sh.tex], sh.brightness);
-  if (dump) dump->rgba = rgba;
-  return rgba;
 }
 
 // Cone of the wave's rays: unit axis through the tile centre, and the sine
@@ -354,9 +347,12 @@ __device__ __forceinline__ bool pass_body_r(const float (&ss)[R], float s_pass, 
 // only reaches through -0 + d * l0 with d of negative sign, so d * (+0) = -0.
 // Edge lanes trace a clamped duplicate pixel (never stored) as the duplicate
 // it is, which keeps the tile cone tight.
-template <int R, bool LIST>
+// DUMP (sfrt_world_trace_points only): the same march and shading, plus a per-ray
+// iteration count and an epilogue writing the float intermediates of listed pixels.
+template <int R, bool LIST, bool DUMP>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
-                                                    const SphereRec* __restrict__ sph) {
+                                                    const SphereRec* __restrict__ sph,
+                                                    DumpArgs dmp) {
   const int lane = threadIdx.x & 63;
   // Adaptive tile order (sfrt_trace.h FrameRec): workgroup 0 may be the sorter.
   const int ntiles = f.tiles_x * ((f.sub_rows + kTile - 1) / kTile);
@@ -385,6 +381,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   const int j = f.ystart + bc * f.yadd;
   const float l0 = f.first_l;
   int draw[R];
+  int iters[R];  // DUMP only: loop trips of :362 per ray, the host's first one included
   float dx[R], dy[R], dz[R], px[R], py[R], pz[R], mv[R], tacc[R];
   // mv: the ray's last step length (> 0 while it marches, +0 once it stopped);
   // `mv > 0` is one compare per step, where a loop-carried bool would be
@@ -398,6 +395,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     py[r] = f.cam[1] + dy[r] * l0;
     pz[r] = f.cam[2] + dz[r] * l0;
     draw[r] = f.first_draw;
+    iters[r] = 1;
     mv[r] = l0 > 0.0f ? 1.0f : 0.0f;
     tacc[r] = l0;  // along-ray distance marched (binary32 sum of the steps)
   }
@@ -458,6 +456,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       px[r] = px[r] + dx[r] * L[r];
       py[r] = py[r] + dy[r] * L[r];
       pz[r] = pz[r] + dz[r] * L[r];
+      if constexpr (DUMP) iters[r] += mv[r] > 0.0f ? 1 : 0;  // a step of a marching ray
       mv[r] = L[r];
       tacc[r] = tacc[r] + L[r];
     }
@@ -600,8 +599,10 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 #pragma unroll
   for (int r = 0; r < R; r++) d[r] = sph[draw[r]];
   Shading sh[R];
+  PixelDump dl[DUMP ? R : 1];
 #pragma unroll
-  for (int r = 0; r < R; r++) sh[r] = shade_texel(f, d[r], px[r], py[r], pz[r], nullptr);
+  for (int r = 0; r < R; r++)
+    sh[r] = shade_texel(f, d[r], px[r], py[r], pz[r], DUMP ? &dl[DUMP ? r : 0] : nullptr);
   uint32_t texel[R];
 #pragma unroll
   for (int r = 0; r < R; r++) texel[r] = f.tex[sh[r].tex];
@@ -609,7 +610,19 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   for (int r = 0; r < R; r++) {
     if (valid(r)) {
       if (sh[r].outside) atomicOr(f.status, 2);  // the reference would read outside the image
-      *px_out(r) = shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
+      const uint32_t rgba = shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
+      *px_out(r) = rgba;
+      if constexpr (DUMP) {
+        const int q = dmp.index[(long long)(b_s - f.sub_row0) * f.sub_w + col(r)];
+        if (q >= 0) {
+          PixelDump& o = dl[r];
+          o.pos[0] = px[r]; o.pos[1] = py[r]; o.pos[2] = pz[r];
+          o.draw = draw[r];
+          o.iters = iters[r];
+          o.rgba = rgba;
+          dmp.out[q] = o;
+        }
+      }
     }
   }
 #endif
@@ -634,53 +647,25 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 // VGPRs (R = 4 needs 60; measured equal to 7 waves when it spilled one, ab/r2_ab10).
 template <int R>
 __global__ __launch_bounds__(64, 8) void k_trace_window_r(InlineArgs args) {
-  trace_tile_window_r<R, false>(args.f, args.s);
+  trace_tile_window_r<R, false, false>(args.f, args.s, DumpArgs{});
 }
 
 // n > 64: the records in device memory (f.spheres, read with scalar loads: rec_at), the
 // culled list per wave.  57 VGPRs at R = 4 (8 waves/SIMD).
 template <int R>
 __global__ __launch_bounds__(64) void k_trace_window_list(FrameRec f) {
-  trace_tile_window_r<R, true>(f, f.spheres);
+  trace_tile_window_r<R, true, false>(f, f.spheres, DumpArgs{});
 }
 
-// Debug/parity kernel: one lane per listed pixel, full sphere list, float
-// intermediates out (pos, drawSphere, iterations, xcoord, ycoord, brightness).
-__global__ __launch_bounds__(256) void k_trace_points(FrameRec f, const int* __restrict__ ij,
-                                                      int count, PixelDump* __restrict__ out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= count) return;
-  const SphereRec* __restrict__ sph = f.spheres;
-  float dx, dy, dz;
-  primary_dir(f, ij[2 * t], ij[2 * t + 1], dx, dy, dz);
-  const float l0 = f.first_l;
-  float px = f.cam[0] + dx * l0, py = f.cam[1] + dy * l0, pz = f.cam[2] + dz * l0;
-  int draw = f.first_draw;
-  int iters = 1;
-  float L = l0;
-  while (L > 0.0f && iters < kMaxIterations) {
-    L = 0.0f;
-    for (int k = 0; k < f.n; k++) {
-      const SphereRec& s = sph[k];
-      const float ex = px - s.cx, ey = py - s.cy, ez = pz - s.cz;
-      const float ss = (ex * ex + ey * ey) + ez * ez;
-      if (ss < s.s_pass) {
-        const float tt = s.r - __builtin_sqrtf(ss);
-        L = L < tt ? tt : L;
-        draw = k;
-      }
-    }
-    px = px + dx * L;
-    py = py + dy * L;
-    pz = pz + dz * L;
-    ++iters;
-  }
-  PixelDump dmp;
-  dmp.pos[0] = px; dmp.pos[1] = py; dmp.pos[2] = pz;
-  dmp.draw = draw;
-  dmp.iters = iters;
-  shade(f, sph[draw], px, py, pz, &dmp);
-  out[t] = dmp;
+// The DUMP instantiations of both (sfrt_world_trace_points): the shipped march and
+// shading, with the float intermediates of listed pixels written out.
+template <int R>
+__global__ __launch_bounds__(64) void k_trace_window_r_dump(InlineArgs args, DumpArgs d) {
+  trace_tile_window_r<R, false, true>(args.f, args.s, d);
+}
+template <int R>
+__global__ __launch_bounds__(64) void k_trace_window_list_dump(FrameRec f, DumpArgs d) {
+  trace_tile_window_r<R, true, true>(f, f.spheres, d);
 }
 
 
@@ -711,6 +696,10 @@ static int trace_rays(const FrameRec& f, bool ordered) {
   return f.n > kPairMinSpheres ? 2 : 1;
 }
 
+const char* trace_build_flavour() {
+  return SFRT_EXP != 0 ? "diagnostic" : kSlots != 2 ? "ab" : SFRT_BUILD_FLAVOUR;
+}
+
 long long trace_tile_key(const FrameRec& f, long long* tiles) {
   *tiles = 0;
   const int rays = trace_rays(f, true);
@@ -721,7 +710,8 @@ long long trace_tile_key(const FrameRec& f, long long* tiles) {
   return (1ll << 62) | ((long long)rays << 56) | (tiles_x << 28) | tiles_y;
 }
 
-int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream) {
+int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream,
+                 const DumpArgs* dump) {
   const long long tiles_y = (f.sub_rows + kTile - 1) / kTile;
   if (tiles_y <= 0 || f.sub_w <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -743,11 +733,27 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
     InlineArgs args;
     args.f = g;
     for (int k = 0; k < f.n; k++) args.s[k] = host_spheres[k];
+    if (dump) {
+      switch (rays) {
+        case 1: hipLaunchKernelGGL(k_trace_window_r_dump<1>, gr, b, 0, s, args, *dump); break;
+        case 2: hipLaunchKernelGGL(k_trace_window_r_dump<2>, gr, b, 0, s, args, *dump); break;
+        case 3: hipLaunchKernelGGL(k_trace_window_r_dump<3>, gr, b, 0, s, args, *dump); break;
+        default: hipLaunchKernelGGL(k_trace_window_r_dump<4>, gr, b, 0, s, args, *dump); break;
+      }
+    } else {
+      switch (rays) {
+        case 1: hipLaunchKernelGGL(k_trace_window_r<1>, gr, b, 0, s, args); break;
+        case 2: hipLaunchKernelGGL(k_trace_window_r<2>, gr, b, 0, s, args); break;
+        case 3: hipLaunchKernelGGL(k_trace_window_r<3>, gr, b, 0, s, args); break;
+        default: hipLaunchKernelGGL(k_trace_window_r<4>, gr, b, 0, s, args); break;
+      }
+    }
+  } else if (dump) {
     switch (rays) {
-      case 1: hipLaunchKernelGGL(k_trace_window_r<1>, gr, b, 0, s, args); break;
-      case 2: hipLaunchKernelGGL(k_trace_window_r<2>, gr, b, 0, s, args); break;
-      case 3: hipLaunchKernelGGL(k_trace_window_r<3>, gr, b, 0, s, args); break;
-      default: hipLaunchKernelGGL(k_trace_window_r<4>, gr, b, 0, s, args); break;
+      case 1: hipLaunchKernelGGL(k_trace_window_list_dump<1>, gr, b, 0, s, g, *dump); break;
+      case 2: hipLaunchKernelGGL(k_trace_window_list_dump<2>, gr, b, 0, s, g, *dump); break;
+      case 3: hipLaunchKernelGGL(k_trace_window_list_dump<3>, gr, b, 0, s, g, *dump); break;
+      default: hipLaunchKernelGGL(k_trace_window_list_dump<4>, gr, b, 0, s, g, *dump); break;
     }
   } else {
     switch (rays) {
@@ -757,14 +763,6 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream)
       default: hipLaunchKernelGGL(k_trace_window_list<4>, gr, b, 0, s, g); break;
     }
   }
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_trace_points(const FrameRec& f, const int* dev_ij, int count, PixelDump* dev_out,
-                        void* stream) {
-  if (count <= 0) return 0;
-  hipLaunchKernelGGL(k_trace_points, dim3((count + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, f, dev_ij, count, dev_out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -16,7 +16,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# SFRT_LIB: another build of the same library (build-flag A/B timing in tools/ only).
+# SFRT_LIB: another build of the same library (build-flag A/B timing in tools/ only;
+# bench.py refuses any library whose build_flavour() is not "release").
 LIB_PATH = os.environ.get("SFRT_LIB") or os.path.join(HERE, "libsfrt.so")
 
 SFRT_OPT_CULL = 1
@@ -37,7 +38,7 @@ ABI_SYMBOLS = (
     "sfrt_world_check", "sfrt_world_trace_points", "sfrt_world_set_option",
     "sfrt_world_submit_frame", "sfrt_world_wait_frame", "sfrt_host_alloc", "sfrt_host_free",
     "sfrt_sort_spheres", "sfrt_deg_to_rad", "sfrt_pass_threshold", "sfrt_error_string",
-    "sfrt_version",
+    "sfrt_version", "sfrt_build_flavour",
     "sfrt_voxel_create", "sfrt_voxel_destroy", "sfrt_voxel_set_size", "sfrt_voxel_set_camera",
     "sfrt_voxel_set_view", "sfrt_voxel_set_blocks", "sfrt_voxel_load_texture",
     "sfrt_voxel_load_dyn_texture", "sfrt_voxel_set_colors", "sfrt_voxel_set_dynamics",
@@ -138,6 +139,7 @@ def lib() -> ctypes.CDLL:
         "sfrt_pass_threshold": ([c_float], c_float),
         "sfrt_error_string": ([c_int], ctypes.c_char_p),
         "sfrt_version": ([], c_int),
+        "sfrt_build_flavour": ([], ctypes.c_char_p),
         "sfrt_voxel_create": ([c_int, P(vp)], c_int),
         "sfrt_voxel_destroy": ([vp], None),
         "sfrt_voxel_set_size": ([vp, c_int, c_int], c_int),
@@ -212,6 +214,11 @@ def sort_spheres(spheres, cam_pos=(0.0, 0.0, 0.0)) -> np.ndarray:
     cam = (ctypes.c_float * 3)(*[float(c) for c in cam_pos])
     _check(lib().sfrt_sort_spheres(s.ctypes.data, s.shape[0], cam), "sfrt_sort_spheres")
     return s
+
+
+def build_flavour() -> str:
+    """sfrt_build_flavour: "release" for the shipped library, "diagnostic" / "ab" otherwise."""
+    return lib().sfrt_build_flavour().decode()
 
 
 def deg_to_rad(deg: float) -> float:

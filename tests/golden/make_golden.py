@@ -5,9 +5,10 @@
 Writes golden.json: per (config, pose) the frame's FNV-1a-64 and SHA-256,
 per-row FNV-1a-64 for frames up to 4K, the march-iteration statistics, and
 ~1000 sampled-pixel float dumps for two configs; plus the full 320x240 frame
-(zlib-compressed RGBA8).  The oracle's iteration statistics are pinned to the
-survey's probe of the unmodified reference by
-tests/test_oracle_golden.py; see DESIGN.md "Parity pinning".
+(zlib-compressed RGBA8).  These are oracle outputs, not reference outputs: the oracle is
+parity unpinned (the reference needs SFML and ships no fixtures).  Its iteration statistics
+match the survey's stub-SFML probe (tests/test_oracle_golden.py), a sanity
+check; see DESIGN.md section 3.
 """
 import hashlib
 import json

@@ -56,7 +56,13 @@ def test_world_create_without_gpu_fails_loudly(lib):
 def test_error_strings(lib):
     for code in range(0, -8, -1):
         assert lib.sfrt_error_string(code)
-    assert lib.sfrt_version() >= 1
+    assert lib.sfrt_version() >= 3
+
+
+def test_in_tree_library_is_release_build(lib):
+    """The shipped libsfrt.so reports the release flavour (bench.py refuses any other:
+    diagnostic -DSFRT_EXP builds write wrong bytes by design, A/B builds carry extra flags)."""
+    assert lib.sfrt_build_flavour() == b"release"
 
 
 def test_deg_to_rad_matches_reference_expression(lib):

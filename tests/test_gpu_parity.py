@@ -190,23 +190,79 @@ def test_row_bands_tile_the_frame(world, floor):
     assert diff_report(f, want, width) == ""
 
 
-@pytest.mark.parametrize("cfg,pose", [("c2_1920x1080_default10", (0.7, 0.3)),
-                                      ("c3_3840x2160_lcg64", (0.0, 0.0))])
-def test_float_intermediates(world, floor, cfg, pose):
-    width, height, sname, _ = scenes.CONFIGS[cfg]
-    scene = scenes.SCENES[sname]().posed(*pose)
-    world.set_scene(scene, width, height)
-    rng = np.random.default_rng(1234)
-    ij = np.stack([rng.integers(0, width, 1000), rng.integers(0, height, 1000)], axis=1)
+def _check_dumps(world, floor, scene, width, height, n, seed, what):
+    rng = np.random.default_rng(seed)
+    ij = np.stack([rng.integers(0, width, n), rng.integers(0, height, n)], axis=1)
+    ij[:4] = [[0, 0], [width - 1, height - 1], [width - 1, 0], [0, height - 1]]  # frame corners
+    ij[4] = ij[5]  # a repeated pixel
     got = world.trace_points(ij)
     orc = oracle_for(scene, width, height, floor)
+    identical = 0
     for (i, j), g in zip(ij.tolist(), got):
         w = orc.dump(i, j)
         assert (g["draw"], g["iters"], g["texel"], g["rgba"]) == \
-               (w["draw"], w["iters"], w["texel"], w["rgba"]), (i, j, g, w)
+               (w["draw"], w["iters"], w["texel"], w["rgba"]), (what, i, j, g, w)
         for k in ("xcoord", "ycoord", "brightness"):
-            assert abs(g[k] - w[k]) <= FLOAT_TOL, (i, j, k, g[k], w[k])
-        assert max(abs(a - b) for a, b in zip(g["pos"], w["pos"])) <= FLOAT_TOL, (i, j)
+            assert abs(g[k] - w[k]) <= FLOAT_TOL, (what, i, j, k, g[k], w[k])
+        assert max(abs(a - b) for a, b in zip(g["pos"], w["pos"])) <= FLOAT_TOL, (what, i, j)
+        identical += all(np.float32(g[k]) == np.float32(w[k]) for k in ("xcoord", "ycoord", "brightness")) \
+            and all(np.float32(a) == np.float32(b) for a, b in zip(g["pos"], w["pos"]))
+    return identical
+
+
+# golden DUMP_CONFIGS (tests/golden/make_golden.py)
+DUMP_CASES = [("c2_1920x1080_default10", (0.7, 0.3)), ("c3_3840x2160_lcg64", (0.0, 0.0))]
+
+
+@pytest.mark.parametrize("cfg,pose", DUMP_CASES)
+@pytest.mark.parametrize("rays", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("order", [1, 0])
+def test_float_intermediates(world, floor, cfg, pose, rays, order):
+    """north_star: float intermediates of SphereWorld.cpp:362-375 (march position, xcoord,
+    ycoord, brightness) within 1e-5 of the oracle, integers (drawSphere, loop trips, texel,
+    RGBA8) exact -- read out of the SHIPPED frame-fill kernel (its DUMP instantiation:
+    sfrt_world_trace_points renders the whole frame through k_trace_window_r<R>), for every
+    tile shape R (0 = the kernel table's pick) in the adaptive tile order (three launches,
+    the last one sorted) and in row-major order."""
+    import sfrt
+    width, height, sname, _ = scenes.CONFIGS[cfg]
+    scene = scenes.SCENES[sname]().posed(*pose)
+    world.set_scene(scene, width, height)
+    world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
+    world.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+    try:
+        same = _check_dumps(world, floor, scene, width, height, 1000, 1234 + rays, (cfg, rays, order))
+    finally:
+        world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
+        world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+    assert same == 1000  # the tolerance is the bar; the floats are in fact identical
+
+
+@pytest.mark.parametrize("rays", [0, 2, 4])
+def test_float_intermediates_list_kernel(world, floor, rays):
+    """n > 64 (256 spheres: the culled-list kernel k_trace_window_list<R>) in the adaptive
+    tile order: the shipped kernel's intermediates against the oracle."""
+    import sfrt
+    scene = scenes.lcg256().posed(1.1, -0.2)
+    world.set_scene(scene, 1600, 1200)
+    world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
+    try:
+        same = _check_dumps(world, floor, scene, 1600, 1200, 600, 99 + rays, ("lcg256", rays))
+    finally:
+        world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
+    assert same == 600
+
+
+def test_trace_points_frame_equals_render(world, floor):
+    """The DUMP instantiation writes the same frame as the shipped kernel: the rgba of every
+    pixel of a small frame out of trace_points equals render()'s bytes."""
+    scene = scenes.lcg64().posed(0.4, 0.2)
+    width, height = 96, 40
+    world.set_scene(scene, width, height)
+    jj, ii = np.mgrid[0:height, 0:width]
+    got = world.trace_points(np.stack([ii.ravel(), jj.ravel()], axis=1))
+    frame = np.array([g["rgba"] for g in got], dtype=np.uint8).ravel()
+    assert diff_report(frame, world.render(), width) == ""
 
 
 def test_camera_outside_every_sphere(world, floor):

@@ -1,14 +1,14 @@
-"""The CPU restatement (oracle/) against its pins and the committed golden fixtures.
+"""The CPU restatement (oracle/) against the survey's sanity checks and the committed golden
+fixtures.
 
-Pins (DESIGN.md "Parity pinning"): the reference cannot be built here (it
-needs SFML), and ships no tests.  The survey ran the unmodified reference TU
-and recorded, per config, the march-iteration statistics of every pixel
-(SURVEY.md 8a, row a2).  Those depend on the scene order, camera basis,
-ray-angle steps, normalisation and the whole march, so reproducing them
-pins everything up to the shading tail.  The shading tail is pinned by the
-exhaustive libm-equivalence of its transcendentals (test_math_exhaustive.py)
-and by its expression-level citation; the survey's frame hashes could not be
-reproduced (its SFML stub is unrecorded) and are listed in DESIGN.md.
+PARITY UNPINNED: the reference cannot be built here (it needs SFML,
+SphereWorld.h:3) and ships no tests or fixtures, so nothing pins the oracle to the reference's
+own output.  The survey ran the reference TU against a stub SFML and recorded, per config, the
+march-iteration statistics of every pixel; reproducing them is a sanity
+check of everything up to the shading tail, not a pin.  The shading tail's transcendentals are
+checked against the host libm exhaustively (test_math_exhaustive.py).  The survey's frame
+hashes from the same stub build do not reproduce (its Image/Color semantics are unrecorded).
+tests/golden/ holds hashes generated from the oracle itself (tests/golden/make_golden.py).
 """
 import json
 import os
