@@ -19,10 +19,14 @@ last tiles drain (the throughput of a double-buffered display or offline loop).
 Before the W warm-up frames, --settle seconds of untimed frames let the chip
 reach its steady clock (it ramps over the first few hundred frames).
 
-Also reported under "also": the 7680x4320 frame row-tiled over the N ranks
-(BASELINE config 4; N = 1, 2, 4, 8) and the 16384x16384 frame on 8 ranks
-(config 5), both strong scaling with the overlapped gather; at N = 1 the
-1920x1080 10-sphere frame (config 2).  And the kernel's HBM roofline from HIP
+Also reported under "also", each line with its own settle (--also-settle), warm-up
+(--also-warmup) and timed frames (--also-steps, independent of --steps so that a short
+headline run still times every line over enough frames): the 7680x4320 frame row-tiled
+over the N ranks (BASELINE config 4; N = 1, 2, 4, 8) and the 16384x16384 frame at N = 1
+and 8 (config 5), strong scaling with the overlapped gather; at N = 1 the 1920x1080
+10-sphere frame (config 2) and variants of the headline; at N > 1 "c_abi_multi", the
+single-process C-ABI path (sfrt_multi_render over devices 0..N-1, RCCL) timed by rank 0
+while the other ranks wait on a host barrier.  And the kernel's HBM roofline from HIP
 events on the launch stream (around every 8th timed frame: a pair per frame
 would put marker packets between all frames of the wall-clock measurement),
 and the CPU baseline: the oracle (CPU restatement, oracle/) rendering one
@@ -170,7 +174,10 @@ def max_over_ranks(x: float) -> float:
 def settle(world, pitch, row0, rows, stream, seconds: float) -> None:
     """Untimed frames until `seconds` have passed: the chip ramps its clock over the
     first few hundred frames after idling, and the timed frames should
-    see the steady state a continuously rendering display or offline job runs at."""
+    see the steady state a continuously rendering display or offline job runs at.  Run
+    before every timed line (the host-side setup between lines lets the clock drop)."""
+    if seconds <= 0 or rows <= 0:
+        return
     buf = torch.empty(rows, pitch, dtype=torch.uint8, device="cuda")
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -276,10 +283,12 @@ def host_delivery(local_rank, floor, scene, width, height, frames, want):
     return res
 
 
-def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, stream):
+def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, stream,
+                  settle_s=0.0):
     """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped transfer)."""
     world.set_scene(scene, width, height)
     pipe, bands = tuned_pipeline(world, rank, world_size, height, width * 4, stream)
+    settle(world, width * 4, pipe.row0, pipe.rows, stream, settle_s)
     wall, kms = time_frames(world, pipe, width * 4, steps, warmup, stream)
     wall = max_over_ranks(wall)
     rays0 = width * pipe.rows
@@ -292,11 +301,12 @@ def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, 
             "bands": bands}
 
 
-# BASELINE.json configs 4 and 5 (and the 8K frame on one GPU): frame size by GPU count.
+# BASELINE.json configs 4 and 5 (the 8K and 16384^2 frames also on one GPU: the
+# strong-scaling anchors of the N > 1 lines): frame size by GPU count.
 # The north star reports Mrays/s at 1080p / 4K / 8K at 1, 2, 4 and 8 GPUs: at N > 1 the
 # 1080p (full scene) and 4K frames are split over the ranks too (at N = 1 they are the
 # headline and the 1920x1080_default10 line).
-EXTRA_FRAMES = {1: [(7680, 4320, "lcg64")],
+EXTRA_FRAMES = {1: [(7680, 4320, "lcg64"), (16384, 16384, "lcg64"), (16384, 16384, "default10")],
                 2: [(1920, 1080, "default10"), (3840, 2160, "lcg64"), (7680, 4320, "lcg64")],
                 4: [(1920, 1080, "default10"), (3840, 2160, "lcg64"), (7680, 4320, "lcg64")],
                 8: [(1920, 1080, "default10"), (3840, 2160, "lcg64"), (7680, 4320, "lcg64"),
@@ -360,6 +370,79 @@ def cpu_baseline(scene, width, height, floor, gpu_frame):
             "at_nproc_threads": at_nproc}
 
 
+def c_abi_multi(devices, floor, frames, steps, warmup, settle_s):
+    """The single-process caller's multi-GPU path (Source.cpp:47-52 fills ONE sf::Image):
+    sfrt_multi_render over `devices` -- one world per device, row bands rendered in parallel,
+    gathered on devices[0] by RCCL (distinct devices) or peer copies (a device listed twice),
+    packed to 3.125 B per pixel for the alpha-binary textures.  Rank 0 times it after the
+    torch.distributed lines while the other ranks wait on a host barrier.  For every frame
+    size: equal, root-weighted and cost-weighted bands x packed / RGBA8 transfers, each after
+    its own settle and warm-up; the last frame of every candidate must equal a one-GPU frame."""
+    n = len(devices)
+    m = sfrt.Multi(devices, sfrt.SFRT_MULTI_AUTO)
+    m.load_texture(*floor)
+    dev0 = torch.device("cuda", devices[0])
+    stream = torch.cuda.Stream(device=dev0)
+    out = {"devices": list(devices),
+           "transport": {sfrt.SFRT_MULTI_RCCL: "rccl", sfrt.SFRT_MULTI_PEER: "peer"}[m.transport]}
+    for fw, fh, sname in frames:
+        scene = scenes.lcg64() if sname == "lcg64" else scenes.SCENES[sname]()
+        m.set_scene(scene, fw, fh)
+        with sfrt.World(devices[0]) as ref:
+            ref.load_texture(*floor)
+            ref.set_scene(scene, fw, fh)
+            want = torch.empty(fh, fw * 4, dtype=torch.uint8, device=dev0)
+            ref.render_band(want.data_ptr(), fw * 4, 0, fh, stream.cuda_stream)
+            ref.check(stream.cuda_stream)
+        bufs = [torch.empty(fh, fw * 4, dtype=torch.uint8, device=dev0) for _ in range(2)]
+        table = {}
+        best = None
+        for weights, f in (("rows", 1.0), ("rows", 2.0), ("rows", 3.0), ("cost", 1.0), ("cost", 2.0)):
+            for fmt in (sfrt.SFRT_TRANSFER_AUTO, sfrt.SFRT_TRANSFER_RGBA):
+                m.set_transfer(fmt)
+                m.set_bands(None)
+                if weights == "rows" and f != 1.0:
+                    m.set_bands([r for _, r in sfrt.multi_bands(fh, n, f)])
+                elif weights == "cost":
+                    m.render(bufs[0].data_ptr(), fw * 4, stream.cuda_stream)  # records the costs
+                    m.check()
+                    m.balance(f)
+
+                def frame(k):
+                    m.render(bufs[k % 2].data_ptr(), fw * 4, stream.cuda_stream)
+                t0 = time.perf_counter()
+                k = 0
+                while time.perf_counter() - t0 < settle_s or k < warmup:
+                    frame(k)
+                    k += 1
+                    if k % 8 == 0:
+                        m.check()
+                m.check()
+                torch.cuda.synchronize(dev0)
+                t0 = time.perf_counter()
+                for k in range(steps):
+                    frame(k)
+                m.check()
+                torch.cuda.synchronize(dev0)
+                wall = time.perf_counter() - t0
+                same = bool(torch.equal(bufs[(steps - 1) % 2], want))
+                packed = m.transfer()[1]
+                key = f"{weights}:{f}/{'packed' if packed else 'rgba8'}"
+                ms = wall / steps * 1e3
+                table[key] = {"ms_per_frame": round(ms, 4), "bit_identical": same}
+                if not same:
+                    raise SystemExit(f"c_abi_multi {fw}x{fh} {key}: frame differs from one GPU")
+                if best is None or ms < best[1]:
+                    best = (key, ms)
+        out[f"{fw}x{fh}_{sname}"] = {
+            "n_gpus": n, "Mrays_per_s": round(fw * fh / (best[1] * 1e-3) / 1e6, 2),
+            "fps": round(1e3 / best[1], 2), "ms_per_frame": round(best[1], 4), "bands": best[0],
+            "candidates": table}
+        del bufs, want
+    m.close()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -367,12 +450,21 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--settle", type=float, default=0.3,
                     help="seconds of untimed frames before the warm-up (clock ramp)")
+    ap.add_argument("--also-steps", type=int, default=200,
+                    help="timed frames of every line under also (at least 20)")
+    ap.add_argument("--also-warmup", type=int, default=20, help="warm-up frames of those lines")
+    ap.add_argument("--also-settle", type=float, default=0.2,
+                    help="seconds of untimed frames before every line under also")
+    ap.add_argument("--c-abi-devices", type=str, default="",
+                    help="devices of the sfrt_multi line (default at N > 1: 0..N-1; e.g. 0,0,0,0 "
+                         "rehearses it on one GPU with peer copies)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the 8K / 16K frames")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline workload (no also lines, no CPU baseline): the command "
                          "whose rocprof kernel trace profiles/*_kernel_stats_by_grid.csv summarises")
     args = ap.parse_args()
+    also_steps, also_warmup = max(20, args.also_steps), max(5, args.also_warmup)
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
@@ -385,8 +477,12 @@ def main() -> None:
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
     torch.cuda.set_device(local_rank)
+    host_group = None
     if world_size > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # a host-side barrier for the c_abi_multi line: ranks waiting on an RCCL barrier
+        # would keep a kernel spinning on the GPUs rank 0 renders on
+        host_group = dist.new_group(backend="gloo")
 
     floor = scenes.load_floor()
     scene = scenes.lcg64()
@@ -403,6 +499,7 @@ def main() -> None:
     settle(w, pitch, *band_of(rank, world_size, height), stream, args.settle)
     pipe, bands = tuned_pipeline(w, rank, world_size, height, pitch, stream)
     row0, rows = pipe.row0, pipe.rows
+    settle(w, pitch, row0, rows, stream, 0.1)  # the tuning's host work let the clock drop
     wall, kernel_ms = time_frames(w, pipe, pitch, args.steps, args.warmup, stream)
     wall = max_over_ranks(wall)
     total_rays = WIDTH * height * args.steps
@@ -436,6 +533,8 @@ def main() -> None:
                        "frames_in_flight": 1},
             "kernel_ms": round(kernel_ms, 4),
             "bands": bands,
+            "library": {"path": os.path.relpath(sfrt.LIB_PATH, ROOT),
+                        "build_flavour": sfrt.build_flavour(), "abi_version": sfrt.lib().sfrt_version()},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None,
@@ -469,22 +568,51 @@ def main() -> None:
     if not (args.no_extra or args.headline_only):
         for fw, fh, sname in EXTRA_FRAMES.get(world_size, []):
             sc_x = scene if sname == "lcg64" else scenes.SCENES[sname]()
-            extra[f"{fw}x{fh}_{sname}"] = measure_frame(w, sc_x, fw, fh, rank, world_size,
-                                                      max(5, args.steps // 2), 2, stream)
+            line = measure_frame(w, sc_x, fw, fh, rank, world_size, also_steps, also_warmup,
+                                 stream, args.also_settle)
+            if world_size == 1:  # one band: the kernel is the frame
+                line["hbm_frac"] = line.pop("hbm_frac_rank0_kernel")
+                line["kernel_ms"] = line.pop("kernel_ms_rank0_band")
+            extra[f"{fw}x{fh}_{sname}"] = line
         w.set_scene(scene, WIDTH, height)
     if rank == 0:
         result["also"] = dict(extra)
+        result["also_timing"] = {"steps": also_steps, "warmup": also_warmup,
+                                 "settle_s": args.also_settle}
+    c_devs = [int(d) for d in args.c_abi_devices.split(",") if d.strip()] if args.c_abi_devices \
+        else (list(range(world_size)) if world_size > 1 else [])
+    if c_devs and not (args.no_extra or args.headline_only):
+        # the single-process multi-GPU path (C ABI), by rank 0 alone while the others wait
+        if rank == 0:
+            frames = [(7680, 4320, "lcg64")] + ([(16384, 16384, "lcg64")] if len(c_devs) >= 8 else [])
+            result["also"]["c_abi_multi"] = c_abi_multi(c_devs, floor, frames, max(20, also_steps // 4),
+                                                        also_warmup, args.also_settle)
+        if host_group is not None:
+            dist.barrier(group=host_group)
     if world_size == 1 and not args.headline_only:
+        def line(wx, fw, fh, name, per_frame=None, in_flight=1, **info):
+            """One N = 1 line under also: its own settle, warm-up and timed frames."""
+            pipe_x = BandPipeline(0, 1, fh, fw * 4, "cuda", local_depth=in_flight)
+            settle(wx, fw * 4, 0, fh, stream, args.also_settle)
+            wall_x, k_x = time_frames(wx, pipe_x, fw * 4, also_steps, also_warmup, stream,
+                                      per_frame=per_frame, in_flight=in_flight)
+            rec = {"n_gpus": 1, "Mrays_per_s": round(fw * fh * also_steps / wall_x / 1e6, 2),
+                   "fps": round(also_steps / wall_x, 2),
+                   "ms_per_frame": round(wall_x / also_steps * 1e3, 4)}
+            if in_flight == 1:
+                rec.update(kernel_ms=round(k_x, 4), hbm_frac=hbm_frac(fw * fh, k_x))
+            else:
+                rec.update(kernel_ms_per_launch_overlapping=round(k_x, 4), frames_in_flight=in_flight,
+                           streams=in_flight)
+            rec.update(info)
+            result["also"][name] = rec
+            del pipe_x
+
         # BASELINE config 2: 1920x1080, 10-sphere scene.
         w2 = sfrt.World(local_rank)
         w2.load_texture(*floor)
         w2.set_scene(scenes.default10(), 1920, 1080)
-        pipe2 = BandPipeline(0, 1, 1080, 1920 * 4, "cuda")
-        wall2, k2 = time_frames(w2, pipe2, 1920 * 4, args.steps, args.warmup, stream)
-        result["also"]["1920x1080_default10"] = {
-            "n_gpus": 1, "Mrays_per_s": round(1920 * 1080 * args.steps / wall2 / 1e6, 2),
-            "fps": round(args.steps / wall2, 2), "kernel_ms": round(k2, 4),
-            "hbm_frac": hbm_frac(1920 * 1080, k2)}
+        line(w2, 1920, 1080, "1920x1080_default10")
         w2.close()
         # BASELINE config 3 with "all textures": every reference texture resident, one
         # per sphere (the per-sphere texture extension; the main line is textures[0]).
@@ -493,19 +621,12 @@ def main() -> None:
             w3.load_texture(rgba, tw, th, slot=slot)
         w3.set_scene(scene, WIDTH, height)
         w3.set_sphere_textures(scenes.all_texture_slots(scene.spheres.shape[0]))
-        pipe3 = BandPipeline(0, 1, height, pitch, "cuda")
-        wall3, k3 = time_frames(w3, pipe3, pitch, args.steps, args.warmup, stream)
-        result["also"]["3840x2160_lcg64_all_textures"] = {
-            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall3 / 1e6, 2),
-            "fps": round(args.steps / wall3, 2), "kernel_ms": round(k3, 4),
-            "hbm_frac": hbm_frac(WIDTH * height, k3)}
+        line(w3, WIDTH, height, "3840x2160_lcg64_all_textures")
         w3.close()
-        del pipe3
         # The adaptive tile order dispatches each frame's tiles longest-first
-        # by the march steps two frames back.  The same workload with a camera turning every
-        # frame (the order always two poses stale), in both orders, and the static camera in
-        # plain row-major order.  Only the camera changes per frame (one C-ABI call).
-        pipe4 = BandPipeline(0, 1, height, pitch, "cuda")
+        # by recorded march steps.  The same workload with a camera turning every frame, in
+        # both orders, and the static camera in plain row-major order.  Only the camera
+        # changes per frame (one C-ABI call).
 
         def turn(k):
             w.set_camera(scene.cam_pos, 0.004 * k, 0.0)
@@ -514,44 +635,25 @@ def main() -> None:
             w.set_scene(scene, WIDTH, height)
             w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
             moving = "turning" in key
-            wall4, k4 = time_frames(w, pipe4, pitch, args.steps, args.warmup, stream,
-                                    per_frame=turn if moving else None)
-            result["also"][key] = {
-                "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall4 / 1e6, 2),
-                "fps": round(args.steps / wall4, 2), "kernel_ms": round(k4, 4),
-                "hbm_frac": hbm_frac(WIDTH * height, k4),
-                "camera": "rotation = 0.004 rad x frame index" if moving else "static pose (0,0)",
-                "tile_order": "adaptive" if order else "row-major (SFRT_OPT_TILE_ORDER 0)"}
+            line(w, WIDTH, height, key, per_frame=turn if moving else None,
+                 camera="rotation = 0.004 rad x frame index" if moving else "static pose (0,0)",
+                 tile_order="adaptive" if order else "row-major (SFRT_OPT_TILE_ORDER 0)")
         w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
         w.set_scene(scene, WIDTH, height)
-        del pipe4
         # Beyond the reference's scene sizes: 256 spheres (the n > 64 kernel).
         w5 = sfrt.World(local_rank)
         w5.load_texture(*floor)
         w5.set_scene(scenes.lcg256(), WIDTH, height)
-        pipe5 = BandPipeline(0, 1, height, pitch, "cuda")
-        wall5, k5 = time_frames(w5, pipe5, pitch, args.steps, args.warmup, stream)
-        result["also"]["3840x2160_lcg256"] = {
-            "n_gpus": 1, "Mrays_per_s": round(WIDTH * height * args.steps / wall5 / 1e6, 2),
-            "fps": round(args.steps / wall5, 2), "kernel_ms": round(k5, 4), "spheres": 256,
-            "hbm_frac": hbm_frac(WIDTH * height, k5)}
+        line(w5, WIDTH, height, "3840x2160_lcg256", spheres=256)
         w5.close()
-        del pipe5
         # Two frames in flight (see frame_streams): the 4K static and 1080p frames.
         for key, (fw, fh, sc2) in (("3840x2160_lcg64_2_in_flight", (WIDTH, height, scene)),
                                    ("1920x1080_default10_2_in_flight", (1920, 1080, scenes.default10()))):
             w6 = sfrt.World(local_rank)
             w6.load_texture(*floor)
             w6.set_scene(sc2, fw, fh)
-            pipe6 = BandPipeline(0, 1, fh, fw * 4, "cuda", local_depth=2)
-            wall6, k6 = time_frames(w6, pipe6, fw * 4, args.steps, args.warmup, stream, in_flight=2)
-            result["also"][key] = {
-                "n_gpus": 1, "Mrays_per_s": round(fw * fh * args.steps / wall6 / 1e6, 2),
-                "fps": round(args.steps / wall6, 2), "ms_per_frame": round(wall6 / args.steps * 1e3, 4),
-                "kernel_ms_per_launch_overlapping": round(k6, 4),
-                "frames_in_flight": 2, "streams": 2}
+            line(w6, fw, fh, key, in_flight=2)
             w6.close()
-            del pipe6
         torch.cuda.synchronize()
         gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()
         result["also"]["3840x2160_lcg64_to_host"] = dict(

@@ -18,6 +18,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -29,7 +30,10 @@ namespace {
 
 // RCCL entry points, resolved from librccl.so.1 by the first RCCL context (a
 // process that already loaded RCCL -- e.g. torch's copy -- gets that one), so
-// the single-GPU library carries no RCCL dependency.
+// the single-GPU library carries no RCCL dependency.  SFRT_RCCL_LIB names another
+// library with the same C API instead: the tests' loopback transport
+// (tests/native/rccl_loopback.cpp), which -- unlike RCCL -- accepts a device listed
+// twice, so the RCCL branch below runs with n > 1 on a one-GPU box.
 struct Rccl {
   decltype(&ncclCommInitAll) comm_init_all = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
@@ -39,14 +43,22 @@ struct Rccl {
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   bool ok = false;
+  bool override_lib = false;  // SFRT_RCCL_LIB: not librccl
 };
 
 const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    void* h = nullptr;
+    const char* alt = getenv("SFRT_RCCL_LIB");
+    if (alt && *alt) {
+      h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+      r.override_lib = true;
+    } else {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (!h) return;
     r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
@@ -439,7 +451,9 @@ int sfrt_multi_create(const int* hip_devices, int n, int transport, sfrt_multi**
     for (int q = 0; q < r; q++) distinct = distinct && hip_devices[q] != hip_devices[r];
   }
   if (transport == SFRT_MULTI_AUTO) transport = distinct ? SFRT_MULTI_RCCL : SFRT_MULTI_PEER;
-  if (transport == SFRT_MULTI_RCCL && (!distinct || !rccl().ok)) return SFRT_E_INVALID;
+  // RCCL refuses a device listed twice (the SFRT_RCCL_LIB loopback does not)
+  if (transport == SFRT_MULTI_RCCL && (!rccl().ok || (!distinct && !rccl().override_lib)))
+    return SFRT_E_INVALID;
   sfrt_multi* m = new sfrt_multi();
   m->transport = transport;
   m->ranks.resize((size_t)n);

@@ -156,6 +156,113 @@ def test_multi_rccl_one_gpu_matches_oracle(floor_tex):
         sfrt.Multi([0, 0], sfrt.SFRT_MULTI_RCCL)
 
 
+def _rccl_loopback_worker(_rank, cases, out_path):
+    """A fresh process whose environment names the loopback transport (SFRT_RCCL_LIB):
+    sfrt_multi's RCCL branch over devices [0] * n, n > 1."""
+    import ctypes
+    import sys
+    for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), os.path.join(ROOT, "oracle"), ROOT):
+        sys.path.insert(0, p)
+    import torch
+    import oracle
+    import scenes as sc
+    import sfrt
+    torch.cuda.set_device(0)
+    floor = sc.load_floor()
+    stats = ctypes.CDLL(os.environ["SFRT_RCCL_LIB"]).rccl_loopback_stats
+    st = (ctypes.c_longlong * 5)()
+    res = []
+    for key, n, mode in cases:
+        m = sfrt.Multi([0] * n, sfrt.SFRT_MULTI_RCCL)
+        assert m.transport == sfrt.SFRT_MULTI_RCCL
+        m.load_texture(*floor)
+        if key == "pipelined":  # six frames queued back to back, camera turning, ragged
+            width, height = 1000, 563
+            scene = sc.lcg64()
+            m.set_scene(scene, width, height)
+            m.set_transfer(sfrt.SFRT_TRANSFER_PACKED if mode == "packed" else sfrt.SFRT_TRANSFER_RGBA)
+            m.set_bands([r for _, r in sfrt.multi_bands(height, n, 2.0)])
+            poses = [(0.3 * k, 0.05 * k - 0.1) for k in range(6)]
+            stream = torch.cuda.Stream()
+            frames = []
+            with torch.cuda.stream(stream):
+                for p in poses:
+                    m.set_camera(scene.cam_pos, *p)
+                    f = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                    m.render(f.data_ptr(), width * 4, stream.cuda_stream)
+                    frames.append(f)
+            m.check()
+            torch.cuda.synchronize()
+            ok = True
+            with sfrt.World(0) as ref:
+                ref.load_texture(*floor)
+                for p, f in zip(poses, frames):
+                    ref.set_scene(scene.posed(*p), width, height)
+                    ok = ok and np.array_equal(f.cpu().numpy().ravel(), ref.render())
+            stats(st)
+            res.append({"case": [key, n, mode], "ok": bool(ok), "stats": list(st),
+                        "packed": m.transfer()[1]})
+            m.close()
+            continue
+        g = GOLDEN["frames"][key]
+        m.set_scene(sc.SCENES[g["scene"]]().posed(*g["pose"]), g["width"], g["height"])
+        kind, fmt = mode.split("/")
+        m.set_transfer(sfrt.SFRT_TRANSFER_PACKED if fmt == "packed" else sfrt.SFRT_TRANSFER_RGBA)
+        hashes = []
+        if kind.startswith("root:"):
+            m.set_bands([r for _, r in sfrt.multi_bands(g["height"], n, float(kind[5:]))])
+        elif kind.startswith("cost:"):
+            hashes.append(oracle.fnv1a64(m.update_image()))  # equal bands, records the costs
+            m.balance(float(kind[5:]))
+        hashes.append(oracle.fnv1a64(m.update_image()))
+        stats(st)
+        res.append({"case": [key, n, mode], "ok": all(h == g["fnv1a64"] for h in hashes),
+                    "stats": list(st), "packed": m.transfer()[1]})
+        m.close()
+    with open(out_path, "w") as fh:
+        json.dump(res, fh)
+
+
+def test_multi_rccl_branch_n_ranks_loopback(floor_tex, tmp_path, monkeypatch):
+    """sfrt_multi's RCCL branch with n = 2, 4 (config 4) and 8 (config 5) ranks: RCCL refuses a
+    device listed twice, so on a one-GPU box the branch runs over the tests' loopback transport
+    (tests/native/rccl_loopback.cpp: the RCCL C API -- ncclCommInitAll, group start/end,
+    ncclGather, ncclSend/ncclRecv -- as HIP peer copies with RCCL's stream ordering) loaded
+    through SFRT_RCCL_LIB.  Equal bands with RGBA8 transfers take the in-place ncclGather;
+    root-weighted and cost-weighted bands the grouped send/recv; packed transfers send the
+    packed bands and unpack on the root.  Every frame hashes to the golden value; six
+    pipelined frames with the camera turning equal one-GPU frames."""
+    import __graft_entry__ as g
+    lib = g.build_loopback()
+    monkeypatch.setenv("SFRT_RCCL_LIB", lib)
+    cases = [("c4_7680x4320_lcg64@0,0", 2, "equal/rgba"), ("c4_7680x4320_lcg64@0,0", 4, "equal/rgba"),
+             ("c4_7680x4320_default10@0,0", 2, "equal/packed"),
+             ("c4_7680x4320_lcg64@0,0", 4, "root:2.5/rgba"), ("c4_7680x4320_default10@0,0", 4, "root:2.0/packed"),
+             ("c4_7680x4320_lcg64@0,0", 4, "cost:1.5/packed"), ("c4_7680x4320_default10@0,0", 2, "cost:1.0/rgba"),
+             ("c5_16384x16384_default10@0,0", 8, "equal/rgba"), ("c5_16384x16384_default10@0,0", 8, "root:2.0/packed"),
+             ("pipelined", 3, "packed"), ("pipelined", 4, "rgba")]
+    out = str(tmp_path / "res.json")
+    mp.start_processes(_rccl_loopback_worker, args=(cases, out), nprocs=1, start_method="spawn",
+                       join=True)
+    res = json.load(open(out))
+    assert len(res) == len(cases)
+    prev = [0] * 5
+    for r, (key, n, mode) in zip(res, cases):
+        assert r["ok"], r
+        d = [a - b for a, b in zip(r["stats"], prev)]
+        prev = r["stats"]
+        packed = mode.endswith("packed")
+        assert r["packed"] == packed, r
+        if mode == "equal/rgba":
+            assert d[0] == n and d[1] == 0, r        # one in-place gather, n posts
+        elif mode.startswith("cost:") and not packed:
+            # the equal-band frame that records the costs gathers; the balanced one sends
+            assert d[0] >= n and d[0] % n == 0 and d[1] == d[2], r
+        else:
+            assert d[0] == 0 and d[1] >= n - 1 and d[1] == d[2], r  # grouped send/recv
+        assert d[3] > 0 and d[4] > 0, r
+
+
 @pytest.mark.parametrize("n,transport", [(1, 1), (3, 2)])
 def test_multi_render_pipelined_frames(floor_tex, n, transport):
     """sfrt_multi_render into device frames on a caller's stream, six frames queued back to
@@ -408,3 +515,46 @@ def test_band_pipeline_packed_frames(floor_tex, monkeypatch, world_size, factor)
         assert np.array_equal(pipes[0].frame(k).cpu().numpy().ravel(), want), k
     for w in worlds:
         w.close()
+
+
+def test_multi_row_costs_after_resize_refused(floor_tex):
+    """A resize invalidates every world's last fill (its rows and tile grid belong to the old
+    frame): sfrt_multi_row_costs / _balance refuse instead of writing past the new frame's
+    rows (7680x4320 on two ranks, then a 1080-row frame)."""
+    import sfrt
+    g = GOLDEN["frames"]["c4_7680x4320_lcg64@0,0"]
+    with _multi([0, 0], sfrt.SFRT_MULTI_PEER, floor_tex) as m:
+        m.set_scene(scenes.SCENES[g["scene"]]().posed(*g["pose"]), g["width"], g["height"])
+        m.update_image()
+        assert m.row_costs().size == g["height"]
+        m.set_scene(scenes.lcg64(), 1920, 1080)
+        with pytest.raises(sfrt.SfrtError) as e:
+            m.balance(1.0)
+        assert e.value.code == -1
+        with pytest.raises(sfrt.SfrtError):
+            m.row_costs()
+        m.update_image()  # a frame of the new size records costs again
+        assert m.row_costs().size == 1080
+
+
+def test_row_costs_invalid_after_unordered_fill(floor_tex):
+    """An ordered render_band records row costs; a later render_band with the tile order off
+    records none, so row_costs refuses (it must not report the earlier band's costs)."""
+    import sfrt
+    import torch
+    w = sfrt.World(0)
+    w.load_texture(*floor_tex)
+    w.set_scene(scenes.lcg64(), 1920, 1080)
+    buf = torch.empty(1080, 1920 * 4, dtype=torch.uint8, device="cuda")
+    w.render_band(buf.data_ptr(), 1920 * 4, 0, 1080)
+    assert w.row_costs()[1].size == 1080
+    w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+    w.render_band(buf.data_ptr(), 1920 * 4, 200, 400)
+    with pytest.raises(sfrt.SfrtError):
+        w.row_costs()
+    w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+    w.render_band(buf.data_ptr(), 1920 * 4, 200, 400)
+    r0, c = w.row_costs()
+    assert (r0, c.size) == (200, 400)
+    w.check()
+    w.close()
