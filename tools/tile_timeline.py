@@ -48,6 +48,16 @@ def main():
                          "slot": int(slot[i])} for i in top],
             "sum_dur_over_8192_slots_us": round(float(dur.sum()) / 8192 / 1e3, 1),
         }
+        # waves in flight per 2 us bin (8192 = every wave slot of the chip busy)
+        edges = np.arange(0.0, float(t1.max()) + 2000.0, 2000.0)
+        started = np.searchsorted(np.sort(t0), edges[:-1] + 1000.0)
+        ended = np.searchsorted(np.sort(t1), edges[:-1] + 1000.0)
+        out[name]["waves_in_flight_per_2us"] = [int(v) for v in started - ended]
+        # tiles finished by the end of each 10 us
+        ends10 = np.arange(10000.0, float(t1.max()) + 10000.0, 10000.0)
+        out[name]["tiles_done_by_10us"] = [int(v) for v in np.searchsorted(np.sort(t1), ends10)]
+        # wave-slot time inside the span that holds no wave, as a fraction of 8192 x span
+        out[name]["idle_slot_frac"] = round(1.0 - float(dur.sum()) / (8192.0 * float(t1.max())), 3)
         print(name, json.dumps(out[name]), flush=True)
     w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
 
