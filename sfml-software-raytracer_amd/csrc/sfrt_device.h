@@ -9,6 +9,16 @@
 
 namespace sfrt {
 
+// v, unchanged, through an empty asm: arithmetic on the result cannot be hoisted above the
+// asm, nor the asm speculated.  Used at the head of a wave-uniform fallback branch (a
+// ballot found some lane outside a fast path's domain) to keep it a branch: left to itself
+// the compiler if-converts such branches -- computing BOTH the fallback and the fast path
+// for every wave and selecting -- which cost ~5 % of the frame kernel's VALU.
+__device__ __forceinline__ float keep_branch(float v) {
+  __asm__ volatile("" : "+v"(v));
+  return v;
+}
+
 // A 64-bit value made wave-uniform (SGPR pair) from lane 0's copy.  The
 // builtin returns int: each half goes through uint32_t so the low word is
 // zero-extended, not sign-extended into the high word.
@@ -294,7 +304,7 @@ constexpr float kTinySqrtArg = 0x1.0p-96f;
 // Correctly rounded sqrtf for any x: the short form unless some lane of the
 // wave has a tiny argument (then the compiler's full lowering for all lanes).
 __device__ __forceinline__ float sqrt_cr(float x) {
-  if (__builtin_amdgcn_ballot_w64(x < kTinySqrtArg)) return __builtin_sqrtf(x);
+  if (__builtin_amdgcn_ballot_w64(x < kTinySqrtArg)) return __builtin_sqrtf(keep_branch(x));
   return sqrt_cr_normal(x);
 }
 

@@ -31,7 +31,8 @@
 // library: -DSFRT_EXP=16 writes per-tile wall-clock start/end into each tile's first
 // pixels, -DSFRT_EXP=32 per-tile march counters (steps, sphere visits, visits that
 // passed for some ray, window/slot mode, culled spheres; tools/visit_counts.py),
-// -DSFRT_EXP=64 skips the shading tail (timing probes; all write wrong bytes).
+// -DSFRT_EXP=64 skips the shading tail, 128 / 256 replace its atan2f / asinf by a multiply
+// (timing probes; all write wrong bytes).
 #ifndef SFRT_EXP
 #define SFRT_EXP 0
 #endif
@@ -63,9 +64,10 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
     dy = div_inrange(y, len, s);
     dz = div_inrange(z, len, s);
   } else {
-    dx = x / len;
-    dy = y / len;
-    dz = z / len;
+    const float l = keep_branch(len);
+    dx = x / l;
+    dy = y / l;
+    dz = z / l;
   }
 }
 
@@ -83,7 +85,11 @@ struct Shading {
 
 __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRec& d, float px,
                                                float py, float pz, PixelDump* dump) {
+#if SFRT_EXP & 128  // timing probe only (wrong bytes): the atan2f call replaced by one multiply
+  float ang = d.atan_c - pz * px;
+#else
   float ang = d.atan_c - atan2f_wave(pz, px);  // == sfrt_math::atan2f (sfrt_device.h)
+#endif
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
   const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
   const float ex = px - d.cx, ey = py - d.cy, ez = pz - d.cz;
@@ -98,10 +104,14 @@ __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRe
     ny = div_inrange(ey, el);
     brightness = div_inrange(3.0f, bd);
   } else {
-    ny = ey / el;
-    brightness = 3.0f / bd;
+    ny = ey / keep_branch(el);
+    brightness = 3.0f / keep_branch(bd);
   }
+#if SFRT_EXP & 256  // timing probe only (wrong bytes): the asinf call replaced by a multiply
+  const float ycoord = sfrt_math::div_pi_plus_half(ny * 0.7f);
+#else
   const float ycoord = sfrt_math::div_pi_plus_half(sfrt_math::asinf(ny));  // == asinf / PI + 0.5f
+#endif
   // fmodf(v, 1.0f) == v - truncf(v) exactly for every binary32 v (NaN/inf -> NaN).
   // texsize of textures[0] (or of the sphere's extension slot), (float)(unsigned) as :376
   const uint32_t tw = d.tex_wh & 0xffffu, th = d.tex_wh >> 16;
@@ -140,6 +150,14 @@ __device__ __forceinline__ uint32_t shade_rgba(uint32_t texel, float brightness)
 // cosine near 1), maximised over the wave, plus slack for binary32 rounding.
 // A tile whose rays spread past ~60 degrees (strided subsets) gets wide = true
 // and is not culled.
+// Square roots of the culling geometry (cone, window): the raw v_sqrt_f32, within 1 ulp of
+// the correctly rounded root for normal arguments (the compiler's sqrtf adds a rescaling for
+// arguments below 2^-96 and a correction step).  Every use is covered by a slack far above
+// 1 ulp: 4e-6 |w| on the cone distances, 1e-5 on the half-angle's sine and relative on the
+// window half-width, plus the absolute cull margin; below 2^-96 the root's absolute error is
+// below 2^-48 either way.
+__device__ __forceinline__ float sqrt_cull(float x) { return __builtin_amdgcn_sqrtf(x); }
+
 struct Cone {
   float ax, ay, az, cos_t, sin_t;
   bool wide;
@@ -180,11 +198,11 @@ __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereR
     const SphereRec s = sph[k];
     if (s.s_pass > 0.0f) {
       const float wx = s.cx - f.cam[0], wy = s.cy - f.cam[1], wz = s.cz - f.cam[2];
-      const float wl = __builtin_sqrtf((wx * wx + wy * wy) + wz * wz);
+      const float wl = sqrt_cull((wx * wx + wy * wy) + wz * wz);
       const float rr = s.r + f.cull_margin + 4e-6f * wl;
       const float t = (wx * c.ax + wy * c.ay) + wz * c.az;
       const float px = wx - t * c.ax, py = wy - t * c.ay, pz = wz - t * c.az;
-      const float perp = __builtin_sqrtf((px * px + py * py) + pz * pz);
+      const float perp = sqrt_cull((px * px + py * py) + pz * pz);
       const bool side = t * c.cos_t + perp * c.sin_t >= -rr;
       const float sa = perp * c.cos_t - t * c.sin_t;  // |w| sin(alpha - theta)
       inc = c.wide || wl <= rr || (side && sa <= rr);
@@ -204,7 +222,7 @@ __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereR
           // for the binary32 error of sa and sb; the product form keeps the root's
           // relative error at a few ulps, and the 1e-5 relative slack covers it.
           const float dmin = fmaxf(0.0f, fminf(sa, sb) - 4e-6f * wl);
-          const float h = __builtin_sqrtf((rr - dmin) * (rr + dmin)) * 1.00001f;
+          const float h = sqrt_cull((rr - dmin) * (rr + dmin)) * 1.00001f;
           const float ext = h + f.cull_margin;
           lo = dn - ext;
           hi = up + ext;
@@ -270,13 +288,13 @@ __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int t
   for (int r = 0; r < R; r++) {
     const float cx = dy[r] * az - dz[r] * ay, cy = dz[r] * ax - dx[r] * az,
                 cz = dx[r] * ay - dy[r] * ax;
-    sin_l = fmaxf(sin_l, __builtin_sqrtf((cx * cx + cy * cy) + cz * cz));
+    sin_l = fmaxf(sin_l, sqrt_cull((cx * cx + cy * cy) + cz * cz));
     wide = wide || ((dx[r] * ax + dy[r] * ay) + dz[r] * az) < 0.5f;
   }
   Cone c;
   c.ax = ax; c.ay = ay; c.az = az;
   c.sin_t = fminf(1.0f, __uint_as_float(wave_max_u32(__float_as_uint(sin_l))) + 1e-5f);
-  c.cos_t = __builtin_sqrtf(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
+  c.cos_t = sqrt_cull(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
   c.wide = __builtin_amdgcn_ballot_w64(wide) != 0;
   return c;
 }
