@@ -468,6 +468,9 @@ def main() -> None:
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    if os.environ.get("SFRT_RCCL_LIB"):
+        raise SystemExit("bench.py measures real RCCL only; SFRT_RCCL_LIB names a test transport "
+                         f"({os.environ['SFRT_RCCL_LIB']}): unset it")
     if sfrt.build_flavour() != "release":
         raise SystemExit(f"bench.py measures the release library only; {sfrt.LIB_PATH} reports "
                          f"build flavour {sfrt.build_flavour()!r} (unset SFRT_LIB, rebuild)")
