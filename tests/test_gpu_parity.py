@@ -502,6 +502,27 @@ def test_random_scenes_match_oracle(world, floor, chunk):
                         f"{width}x{height}): {msg}"
 
 
+@pytest.mark.parametrize("rays", [4, 3])
+def test_random_scenes_match_oracle_wide_tiles(world, floor, rays):
+    """The 4K headline's tile shapes on random scenes: R = 4 (32x8 tiles, the kernel the
+    adaptive order picks for large frames) and R = 3 (24x8) forced on 150 scenes each (the
+    default table gives these small frames 16x8 or 8x8 tiles), through update_image, vs the
+    oracle byte for byte."""
+    import sfrt
+    world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
+    try:
+        for seed in range(1000 + 150 * rays, 1000 + 150 * rays + 150):
+            sc, width, height = _fuzz_scene(seed)
+            world.set_scene(sc, width, height)
+            got = world.render()
+            want = oracle_for(sc, width, height, floor).render(host_threads())
+            msg = diff_report(got, want, width)
+            assert not msg, f"R={rays} seed {seed} ({sc.spheres.shape[0]} spheres, cam {sc.cam_pos}, " \
+                            f"{width}x{height}): {msg}"
+    finally:
+        world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
+
+
 def test_random_subsets_match_oracle(world, floor):
     """UpdateImage(ystart, yadd, xstart, xadd) pixel subsets of random scenes (SphereWorld.cpp:94,97),
     on a poisoned canvas: the same bytes as the oracle's, and no other byte touched."""
