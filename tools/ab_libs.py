@@ -69,7 +69,17 @@ def child(cases, reps, rays):
         torch.cuda.synchronize()
         w.check(stream.cuda_stream)
         t = sorted(a.elapsed_time(b) for a, b in ev)
-        out[name] = {"us": round((t[len(t) // 2] - gap) * 1e3, 2),
+        # the same frames back to back with no markers between them: wall time per frame
+        # (kernel plus the launch boundary a frame loop pays)
+        import time
+        t0 = time.perf_counter()
+        for k in range(reps):
+            if turn:
+                w.set_camera(sc.cam_pos, 0.004 * (20 + reps + k), 0.0)
+            w.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / reps
+        out[name] = {"us": round((t[len(t) // 2] - gap) * 1e3, 2), "wall_us": round(wall * 1e6, 2),
                      "fnv": oracle.fnv1a64(buf.cpu().numpy())}
     print("RESULT " + json.dumps(out), flush=True)
 
@@ -89,6 +99,7 @@ def main():
         return
     libs = a.libs.split(",")
     res = {lib: {c: [] for c in cases} for lib in libs}
+    walls = {lib: {c: [] for c in cases} for lib in libs}
     hashes = {}
     for rnd in range(a.rounds):
         for lib in libs:  # "path" or "path@R" (R = SFRT_OPT_RAYS_PER_LANE); "path!" = timing probe
@@ -108,6 +119,7 @@ def main():
             d = json.loads(line[0][7:])
             for c in cases:
                 res[lib][c].append(d[c]["us"])
+                walls[lib][c].append(d[c].get("wall_us", 0.0))
                 if probe:
                     continue  # a probe build writes other bytes by design
                 hashes.setdefault(c, d[c]["fnv"])
@@ -117,7 +129,10 @@ def main():
     for lib in libs:
         summary[lib] = {c: sorted(v)[len(v) // 2] for c, v in res[lib].items()}
         print(f"{lib:40s} " + "  ".join(f"{c} {summary[lib][c]:8.2f}" for c in cases))
-    print(json.dumps({"median_us": summary, "rounds": res, "bytes_identical": True}))
+    wsum = {lib: {c: sorted(v)[len(v) // 2] for c, v in walls[lib].items()} for lib in libs}
+    for lib in libs:
+        print(f"wall {lib:35s} " + "  ".join(f"{c} {wsum[lib][c]:8.2f}" for c in cases))
+    print(json.dumps({"median_us": summary, "median_wall_us": wsum, "rounds": res, "bytes_identical": True}))
 
 
 if __name__ == "__main__":
