@@ -300,6 +300,49 @@ __device__ __forceinline__ Cone tile_cone_r(const FrameRec& f, int tile_x, int t
 }
 
 
+// The same cone from the tile's four corner rays only.  Restricted to the image plane
+// {fwd + right h + up v}, the angle to the axis has convex sublevel sets below 90 degrees (a
+// convex circular cone cut by a plane), so over the tile's rectangle of (h, v) it is largest
+// at a corner; every ray of the tile, edge duplicates included, lies in that rectangle (h and
+// v are monotone in the pixel indices, also after rounding).  So if every corner ray is
+// within 60 degrees of the axis, so is every ray, and the largest corner sine plus the same
+// 1e-5 slack bounds every ray's (the slack covers the binary32 error of the corners' and of
+// the rays' directions, a few 1e-8); otherwise the tile is wide.  Lane l computes corner l % 4.
+template <int R>
+__device__ __forceinline__ Cone tile_cone_corners(const FrameRec& f, int tile_x, int tile_y, int lane) {
+  const float ic = (float)f.xstart +
+                   ((float)(tile_x * R * kTile) + (0.5f * (float)(R * kTile) - 0.5f)) * (float)f.xadd;
+  const float jc = (float)f.ystart +
+                   ((float)(f.sub_row0 + tile_y * kTile) + 3.5f) * (float)f.yadd;
+  const float hc = f.h_start + f.h_inc * ic;
+  const float vc = f.v_start + jc * f.v_inc;
+  float ax = (f.fwd[0] + f.right[0] * hc) + f.up[0] * vc;
+  float ay = (f.fwd[1] + f.right[1] * hc) + f.up[1] * vc;
+  float az = (f.fwd[2] + f.right[2] * hc) + f.up[2] * vc;
+  const float inv = __builtin_amdgcn_rsqf((ax * ax + ay * ay) + az * az);
+  ax *= inv; ay *= inv; az *= inv;
+  // corner lane % 4: column 0 or 8R - 1, row 0 or 7 of the tile, clamped like the rays
+  const int a0 = tile_x * R * kTile + ((lane & 1) ? R * kTile - 1 : 0);
+  const int b0 = f.sub_row0 + tile_y * kTile + ((lane & 2) ? kTile - 1 : 0);
+  const int a = a0 < f.sub_w ? a0 : f.sub_w - 1;
+  const int b = b0 < f.sub_row0 + f.sub_rows ? b0 : f.sub_row0 + f.sub_rows - 1;
+  const float h = f.h_start + f.h_inc * (float)(f.xstart + a * f.xadd);
+  const float v = f.v_start + (float)(f.ystart + b * f.yadd) * f.v_inc;
+  float x = (f.fwd[0] + f.right[0] * h) + f.up[0] * v;
+  float y = (f.fwd[1] + f.right[1] * h) + f.up[1] * v;
+  float z = (f.fwd[2] + f.right[2] * h) + f.up[2] * v;
+  const float il = __builtin_amdgcn_rsqf((x * x + y * y) + z * z);
+  x *= il; y *= il; z *= il;
+  const float cx = y * az - z * ay, cy = z * ax - x * az, cz = x * ay - y * ax;
+  const float sin_l = sqrt_cull((cx * cx + cy * cy) + cz * cz);
+  Cone c;
+  c.ax = ax; c.ay = ay; c.az = az;
+  c.sin_t = fminf(1.0f, __uint_as_float(wave_max_u32(__float_as_uint(sin_l))) + 1e-5f);
+  c.cos_t = sqrt_cull(fmaxf(0.0f, 1.0f - c.sin_t * c.sin_t));
+  c.wide = __builtin_amdgcn_ballot_w64(!(((x * ax + y * ay) + z * az) >= 0.5f)) != 0;
+  return c;
+}
+
 // L = +0 for a lane's R rays at the start of a march step, two registers per
 // v_mov_b64 (left to itself the compiler copies one zero register into three
 // others and then pairs them: five moves a step for R = 4, not two).
@@ -429,7 +472,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   float lo = -__builtin_inff(), hi = __builtin_inff();
   int cidx = lane;        // sphere of culled-list entry `lane`
   if (windowed) {
-    const Cone cone = tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
+    // R >= 3: four corner rays per wave are cheaper than R rays per lane (profiles/ab/r3_ab9)
+    const Cone cone = R >= 3 ? tile_cone_corners<R>(f, tile_x, tile_y, lane)
+                             : tile_cone_r<R>(f, tile_x, tile_y, dx, dy, dz);
     if (!LIST) {
       m = cull_window(f, sph, 0, cone, lo, hi);
     } else {
