@@ -275,6 +275,35 @@ def test_camera_outside_every_sphere(world, floor):
     assert diff_report(got, want, 160) == ""
 
 
+@pytest.mark.parametrize("case", ["far2^40", "far2^100", "tiny2^-30"])
+def test_extreme_scale_scene_matches_oracle(world, floor, case):
+    """Extreme coordinates, in both tile orders, against the oracle: sphere 0 of the default
+    scene moved to ~2^40 or ~2^100 (sphere 0 is drawSphere for rays that leave every sphere,
+    so the shading tail's division guards see huge or infinite operands, and the 2^100 frame
+    has a non-finite reach: no culling), and the whole scene scaled by 2^-30 (every radius
+    below the 0.01 pass threshold).  Scaling the whole scene up does not work as a test: at
+    ~2^37 a step smaller than half an ulp of the position leaves it unchanged and the
+    reference's loop (SphereWorld.cpp:362-371) never ends -- the oracle's neither."""
+    import sfrt
+    base = scenes.default10()
+    sp = base.spheres.copy()
+    cam = base.cam_pos
+    if case == "tiny2^-30":
+        sp[:, :4] *= np.float32(2.0 ** -30)
+        cam = tuple(float(v) * 2.0 ** -30 for v in cam)
+    else:
+        far = 2.0 ** (40 if case == "far2^40" else 100)
+        sp[0, :3] = np.float32([far, -far / 2, far])
+    scene = scenes.Scene(f"default10_{case}", sp, cam_pos=cam)
+    want = oracle_for(scene, 192, 108, floor).render(host_threads())
+    for order in (0, 1):
+        world.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
+        world.set_scene(scene, 192, 108)
+        got = world.render()
+        assert diff_report(got, want, 192) == "", f"{case}, tile order {order}"
+    world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+
+
 @pytest.mark.parametrize("pose", [(0.0, 0.0), (1.1, -0.2)])
 def test_lcg256_ordered_frames_match_oracle(world, floor, pose):
     """256 spheres (the culled-list kernel, 32x8 tiles at 1600 x 1200 in the adaptive tile
