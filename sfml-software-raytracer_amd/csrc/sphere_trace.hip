@@ -121,7 +121,9 @@ __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRe
   w = (w - __builtin_truncf(w)) * (float)th;
   // float -> unsigned: v_cvt_u32_f32 (NaN -> 0), as x86's cvttss2si for [0, 2^31).
   const uint32_t tx = __float2uint_rz(u), ty = __float2uint_rz(w);
-  const uint32_t idx = tx + ty * tw;
+  // ty < th <= 0xffff (a fraction in [0, 1) times th, or 0 from NaN; radii are > 0, so no
+  // negative fraction reaches -1 / th): the 24-bit multiply is the exact product
+  const uint32_t idx = tx + __umul24(ty, tw);
   Shading sh;
   sh.outside = !(idx < tw * th);
   sh.tex = d.tex_off + (sh.outside ? 0u : idx);
@@ -647,7 +649,10 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   const int b_s = f.sub_row0 + tile_y * kTile + (lane_s >> 3);
   auto col = [&](int r) { return tile_x * R * kTile + r * kTile + (lane_s & 7); };
   auto valid = [&](int r) { return col(r) < f.sub_w && b_s < b_end; };
-  auto px_out = [&](int r) { return f.out + (long long)(b_s - f.sub_row0) * f.out_pitch + col(r); };
+  // the row's first pixel, once per lane (inside each slot's store branch the compiler
+  // recomputed the 64-bit row offset, three quarter-rate multiplies per slot)
+  uint32_t* const row_out = f.out + (long long)(b_s - f.sub_row0) * f.out_pitch;
+  auto px_out = [&](int r) { return row_out + col(r); };
 #if SFRT_EXP & 64  // timing probe only (wrong bytes): the march without the shading tail
 #pragma unroll
   for (int r = 0; r < R; r++)
@@ -660,7 +665,8 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   // (same values as the real pixel) and store nothing.
   SphereRec d[R];
 #pragma unroll
-  for (int r = 0; r < R; r++) d[r] = sph[draw[r]];
+  for (int r = 0; r < R; r++)  // draw < n <= 1024: a 32-bit byte offset from the records' base
+    d[r] = *(const SphereRec*)((const char*)sph + (uint32_t)draw[r] * (uint32_t)sizeof(SphereRec));
   Shading sh[R];
   PixelDump dl[DUMP ? R : 1];
 #pragma unroll
