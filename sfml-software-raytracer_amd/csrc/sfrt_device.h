@@ -105,6 +105,14 @@ __device__ __forceinline__ bool div_operand_ok(float v) {
   return __builtin_fabsf(v) >= 0x1.0p-40f && __builtin_fabsf(v) < 0x1.0p40f;
 }
 
+// The wave's lanes whose v fails div_operand_ok, as the OR of one ballot per compare: a
+// ballot of a combined condition costs two more VALU (the compiler turns the lane mask back
+// into a value and compares it again), a ballot of one compare is that compare's own mask.
+__device__ __forceinline__ uint64_t ballot_bad_operand(float v) {
+  return __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(v) >= 0x1.0p-40f)) |
+         __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(v) < 0x1.0p40f));
+}
+
 // atan2f(y, x), bit for bit sfrt_math::atan2f (= glibc's e_atan2f.c), with a
 // cheaper path for the waves the renderers produce.  When every lane of the
 // wave has finite non-zero x and y and |y/x| in [2^-29, 2^25), no special case
@@ -123,9 +131,10 @@ __device__ __forceinline__ float atan2f_wave(float y, float x) {
   // all rare, takes the general code, like one with |y/x| outside [2^-29, 2^25))
   const float q = div_inrange(y, x);
   const uint32_t iq = f2u(q) & 0x7fffffffu;
-  const bool general = div_operand_ok(x) && div_operand_ok(y) &&
-                       (iq - 0x31000000u < 0x4c000000u - 0x31000000u);
-  if (__builtin_amdgcn_ballot_w64(!general)) return sfrt_math::atan2f(y, x);
+  // (ballot_bad_operand: one ballot per compare)
+  if (ballot_bad_operand(x) | ballot_bad_operand(y) |
+      __builtin_amdgcn_ballot_w64(!(iq - 0x31000000u < 0x4c000000u - 0x31000000u)))
+    return sfrt_math::atan2f(y, x);
   const float a = u2f(iq);
   const int id = iq < 0x3ee00000u ? -1
                : iq < 0x3f300000u ? 0

@@ -58,7 +58,7 @@ __device__ __forceinline__ void primary_dir(const FrameRec& f, int i, int j, flo
   const float len = sqrt_cr_normal((x * x + y * y) + z * z);
   // components in [2^-40, 2^40) put len there too: one shared reciprocal seed
   // (div_inrange, the same bits as `/`); a wave with a zero component takes `/`
-  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(x) && div_operand_ok(y) && div_operand_ok(z))) == 0) {
+  if ((ballot_bad_operand(x) | ballot_bad_operand(y) | ballot_bad_operand(z)) == 0) {
     const float s = div_seed(len);
     dx = div_inrange(x, len, s);
     dy = div_inrange(y, len, s);
@@ -100,7 +100,7 @@ __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRe
   // ey / el and 3 / bd through div_inrange (same bits) unless some lane's operands
   // leave [2^-40, 2^40) (bd >= 3 needs only the upper bound)
   float ny, brightness;
-  if (__builtin_amdgcn_ballot_w64(!(div_operand_ok(ey) && div_operand_ok(el) && bd < 0x1.0p40f)) == 0) {
+  if ((ballot_bad_operand(ey) | ballot_bad_operand(el) | __builtin_amdgcn_ballot_w64(!(bd < 0x1.0p40f))) == 0) {
     ny = div_inrange(ey, el);
     brightness = div_inrange(3.0f, bd);
   } else {
