@@ -1,6 +1,9 @@
 """Diagnostic: per-tile wall-clock start/end of the sphere kernel (a build with
 -DSFRT_EXP=16 writes them into pixels 0-3 of each tile's first row; wrong image bytes).
     SFRT_LIB=sfml-software-raytracer_amd/build_x16/libsfrt.so python tools/tile_timeline.py [--1080]
+        [--rays 2] [--dump DIR]
+--rays forces the pixels per lane of the 4K frame (SFRT_OPT_RAYS_PER_LANE); --dump saves each case's
+per-tile start, end and trips (tile order) as DIR/<case>_r<R>.npz.
 Prints the kernel's span, the distribution of tile durations, and when the longest
 tiles start and end, for a static and a turning camera."""
 import json
@@ -19,9 +22,14 @@ def main():
     # --1080: the 1920x1080 10-sphere frame (16x8 tiles in the adaptive order)
     W, H, R, sc = (1920, 1080, 2, scenes.default10()) if "--1080" in sys.argv else \
         (3840, 2160, 4, scenes.lcg64())
+    if "--rays" in sys.argv:
+        R = int(sys.argv[sys.argv.index("--rays") + 1])
+    dump = sys.argv[sys.argv.index("--dump") + 1] if "--dump" in sys.argv else None
     stream = torch.cuda.Stream()
     w = sfrt.World(0)
     w.load_texture(*scenes.load_floor())
+    if "--rays" in sys.argv:
+        w.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, R)
     out = {}
     for name, turn, order in (("static", False, 1), ("turning", True, 1), ("static_rowmajor", False, 0)):
         w.set_scene(sc, W, H)
@@ -39,6 +47,9 @@ def main():
         t0 = (t0 - base) * 10  # ns (100 MHz)
         t1 = (t1 - base) * 10
         dur = t1 - t0
+        if dump:
+            os.makedirs(dump, exist_ok=True)
+            np.savez(os.path.join(dump, f"{name}_r{R}.npz"), t0=t0, t1=t1, trips=trips, slot=slot)
         top = np.argsort(-dur)[:10]
         out[name] = {
             "span_us": round(float(t1.max()) / 1e3, 1),
@@ -60,6 +71,7 @@ def main():
         out[name]["idle_slot_frac"] = round(1.0 - float(dur.sum()) / (8192.0 * float(t1.max())), 3)
         print(name, json.dumps(out[name]), flush=True)
     w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+    w.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 0)
 
 
 if __name__ == "__main__":
