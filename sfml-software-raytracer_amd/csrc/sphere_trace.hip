@@ -417,6 +417,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
                                                     const SphereRec* __restrict__ sph,
                                                     DumpArgs dmp) {
   const int lane = threadIdx.x & 63;
+#if SFRT_EXP & 512  // with 16: the wave's entry time in place of its slot (wrong bytes)
+  const uint64_t dbg_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   // Adaptive tile order (sfrt_trace.h FrameRec): workgroup 0 may be the sorter.
   const int ntiles = f.tiles_x * ((f.sub_rows + kTile - 1) / kTile);
   int slot = (int)blockIdx.x;
@@ -706,7 +709,12 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
   if (lane < 4 && valid(0)) {
     const uint32_t v = lane == 0 ? (uint32_t)dbg_t0 : lane == 1 ? (uint32_t)dbg_t1
-                     : lane == 2 ? (uint32_t)trips : (uint32_t)slot;
+                     : lane == 2 ? (uint32_t)trips
+#if SFRT_EXP & 512
+                     : (uint32_t)dbg_entry;
+#else
+                     : (uint32_t)slot;
+#endif
     *px_out(0) = v;
   }
 #endif

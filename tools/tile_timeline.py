@@ -1,9 +1,10 @@
 """Diagnostic: per-tile wall-clock start/end of the sphere kernel (a build with
 -DSFRT_EXP=16 writes them into pixels 0-3 of each tile's first row; wrong image bytes).
     SFRT_LIB=sfml-software-raytracer_amd/build_x16/libsfrt.so python tools/tile_timeline.py [--1080]
-        [--rays 2] [--dump DIR]
+        [--rays 2] [--dump DIR] [--entry]
 --rays forces the pixels per lane of the 4K frame (SFRT_OPT_RAYS_PER_LANE); --dump saves each case's
-per-tile start, end and trips (tile order) as DIR/<case>_r<R>.npz.
+per-tile start, end and trips (tile order) as DIR/<case>_r<R>.npz; --entry (a -DSFRT_EXP=528 build)
+reports the time from the wave's entry to its tile start.
 Prints the kernel's span, the distribution of tile durations, and when the longest
 tiles start and end, for a static and a turning camera."""
 import json
@@ -47,6 +48,11 @@ def main():
         t0 = (t0 - base) * 10  # ns (100 MHz)
         t1 = (t1 - base) * 10
         dur = t1 - t0
+        if "--entry" in sys.argv:  # -DSFRT_EXP=528 build: the slot field holds the entry time
+            ent = (slot - base) * 10
+            pro = t0 - ent
+            print(name, "entry_to_tile_start_us_p10_p50_p90_p99",
+                  [round(float(np.percentile(pro, q)) / 1e3, 2) for q in (10, 50, 90, 99)], flush=True)
         if dump:
             os.makedirs(dump, exist_ok=True)
             np.savez(os.path.join(dump, f"{name}_r{R}.npz"), t0=t0, t1=t1, trips=trips, slot=slot)
