@@ -240,9 +240,12 @@ __device__ __forceinline__ uint64_t cull_window(const FrameRec& f, const SphereR
 // event of the launch that read it), and wave-uniform loads from that space are scalar
 // loads -- through the generic pointer the compiler must assume the frame's stores may
 // alias them and emits vector loads into VGPRs (the n > 64 kernel's records).
-__device__ __forceinline__ SphereRec rec_at(const SphereRec* p, int k) {
+// k is unsigned and < 2^27, so k * 32 is a 32-bit byte offset the scalar load takes as its
+// SGPR offset (a signed index costs a 64-bit shift and add per record).
+__device__ __forceinline__ SphereRec rec_at(const SphereRec* p, uint32_t k) {
   const __attribute__((address_space(4))) uint32_t* q =
-      (const __attribute__((address_space(4))) uint32_t*)(p + k);
+      (const __attribute__((address_space(4))) uint32_t*)(
+          (const __attribute__((address_space(4))) char*)p + k * (uint32_t)sizeof(SphereRec));
   uint32_t w[sizeof(SphereRec) / 4];
 #pragma unroll
   for (int i = 0; i < (int)(sizeof(SphereRec) / 4); i++) w[i] = q[i];
@@ -440,6 +443,9 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
 #if SFRT_EXP & 16  // diagnostic build: per-tile wall-clock start/end (wrong bytes)
   const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
+#if SFRT_EXP & 1024  // and the tile's shader clocks (s_memtime) in place of its trips
+  const uint64_t dbg_c0 = __builtin_amdgcn_s_memtime();
+#endif
 #endif
   const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
   const int b_end = f.sub_row0 + f.sub_rows;
@@ -515,7 +521,16 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
   }
   // sphere of culled entry e (wave-uniform)
-  auto entry = [&](int e) { return LIST ? __builtin_amdgcn_readlane(cidx, e) : e; };
+  auto entry = [&](uint32_t e) { return LIST ? (uint32_t)__builtin_amdgcn_readlane(cidx, (int)e) : e; };
+  // First set bit of a 64-bit culling mask, 63 for an empty mask (s_ff1 gives -1): entry 63 is
+  // always readable -- a record of the n <= 64 kernel's argument block, or lane 63 of the list
+  // (its sphere, or sphere 63 < n) -- so a lookahead past the last entry loads a record it never uses.
+  auto first_entry = [](uint64_t x) -> uint32_t {
+    uint32_t e;
+    __asm__("s_ff1_i32_b64 %0, %1" : "=s"(e) : "s"(x));
+    return e & 63u;
+  };
+  auto clear_entry = [](uint64_t x, uint32_t e) -> uint64_t { return x & ~(1ull << e); };  // s_bitset0
 
   // pos += dir * L (SphereWorld.cpp:371) on every lane (see above)
   auto advance = [&](const float (&L)[R]) {
@@ -615,23 +630,26 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
           m & __builtin_amdgcn_ballot_w64(lo < thi) & __builtin_amdgcn_ballot_w64(hi > tlo);
       // The visits, in index order, each issuing the next record's scalar loads
       // before its own arithmetic (the loads' latency hides under the R rays'
-      // distance tests; kn = k for the last visit reloads a record already in
-      // the scalar cache).
+      // distance tests; past the last entry the lookahead loads entry 63's record,
+      // unused).  Scalar work per visit is kept short: the scalar unit is shared by
+      // the CU's four SIMDs (profiles/r3y_salu_mix_check.txt).
       if (win) {
-        uint64_t mm = win;
-        int k = entry(__builtin_ctzll(mm));
-        mm &= mm - 1;
+        uint32_t e = first_entry(win);
+        uint64_t mm = clear_entry(win, e);
+        uint32_t k = entry(e);
         const SphereRec s0 = rec_at(sph, k);
         float cx = s0.cx, cy = s0.cy, cz = s0.cz, rad = s0.r, sp = s0.s_pass;
-        for (;;) {
-          const int kn = mm ? entry(__builtin_ctzll(mm)) : k;
+        bool more;
+        do {  // the exit test at the bottom: a mid-loop exit made the back edge ~18 scalar ops
+          const uint32_t en = first_entry(mm);
+          const uint32_t kn = entry(en);
           const SphereRec sn = rec_at(sph, kn);
           const float ncx = sn.cx, ncy = sn.cy, ncz = sn.cz, nr = sn.r, nsp = sn.s_pass;
-          visit(cx, cy, cz, rad, sp, k, L);
-          if (!mm) break;
-          mm &= mm - 1;
+          visit(cx, cy, cz, rad, sp, (int)k, L);
+          more = mm != 0;
+          mm = clear_entry(mm, en);
           k = kn; cx = ncx; cy = ncy; cz = ncz; rad = nr; sp = nsp;
-        }
+        } while (more);
       }
       advance(L);
     }
@@ -707,9 +725,14 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
 #endif
 #if SFRT_EXP & 16
   const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
+#if SFRT_EXP & 1024
+  const uint32_t dbg_trips = (uint32_t)(__builtin_amdgcn_s_memtime() - dbg_c0);
+#else
+  const uint32_t dbg_trips = (uint32_t)trips;
+#endif
   if (lane < 4 && valid(0)) {
     const uint32_t v = lane == 0 ? (uint32_t)dbg_t0 : lane == 1 ? (uint32_t)dbg_t1
-                     : lane == 2 ? (uint32_t)trips
+                     : lane == 2 ? dbg_trips
 #if SFRT_EXP & 512
                      : (uint32_t)dbg_entry;
 #else

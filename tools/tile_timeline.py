@@ -1,10 +1,11 @@
 """Diagnostic: per-tile wall-clock start/end of the sphere kernel (a build with
 -DSFRT_EXP=16 writes them into pixels 0-3 of each tile's first row; wrong image bytes).
     SFRT_LIB=sfml-software-raytracer_amd/build_x16/libsfrt.so python tools/tile_timeline.py [--1080]
-        [--rays 2] [--dump DIR] [--entry]
+        [--rays 2] [--dump DIR] [--entry] [--clock]
 --rays forces the pixels per lane of the 4K frame (SFRT_OPT_RAYS_PER_LANE); --dump saves each case's
 per-tile start, end and trips (tile order) as DIR/<case>_r<R>.npz; --entry (a -DSFRT_EXP=528 build)
-reports the time from the wave's entry to its tile start.
+reports the time from the wave's entry to its tile start; --clock (a -DSFRT_EXP=1040 build) the
+shader clock over each tile (its s_memtime clocks over its s_memrealtime span).
 Prints the kernel's span, the distribution of tile durations, and when the longest
 tiles start and end, for a static and a turning camera."""
 import json
@@ -48,6 +49,11 @@ def main():
         t0 = (t0 - base) * 10  # ns (100 MHz)
         t1 = (t1 - base) * 10
         dur = t1 - t0
+        if "--clock" in sys.argv:  # -DSFRT_EXP=1040 build: the trips field holds the tile's s_memtime clocks
+            ghz = trips / np.maximum(dur, 1) 
+            wsum = float((trips).sum()) / float(dur.sum())
+            print(name, "shader_clock_GHz_p10_p50_p90_weighted",
+                  [round(float(np.percentile(ghz, q)), 3) for q in (10, 50, 90)] + [round(wsum, 3)], flush=True)
         if "--entry" in sys.argv:  # -DSFRT_EXP=528 build: the slot field holds the entry time
             ent = (slot - base) * 10
             pro = t0 - ent
