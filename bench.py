@@ -57,6 +57,11 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # 2.4 GHz = 1.229e12 wave-instructions/s (x 64 lanes = the 157.3 TFLOPS FP32
 # figure counted as FMA = 2).
 VALU_PEAK_WAVE_INSTS = 256 * 4 * 0.5 * 2.4e9
+# What a plain stream of independent v_add_f32 reaches on this chip at 8 waves/SIMD: 0.438
+# wave64 instructions per SIMD-clock (tools/native/pk_rate_check.hip), at the 2.33 GHz shader
+# clock measured across the headline kernel's tiles (s_memtime over s_memrealtime, the
+# -DSFRT_EXP=1040 build): profiles/r3y_valu_rate_check.txt, r3y_timeline/tile_timeline_4k_clock.txt.
+VALU_STREAM_CEILING = 256 * 4 * 0.438 * 2.33e9
 BYTES_PER_RAY = 4            # RGBA8 store; texture + sphere table are cache-resident
 WIDTH, ROWS_PER_GPU = 3840, 2160
 
@@ -554,6 +559,8 @@ def main() -> None:
                 result["valu_roofline"] = {
                     "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTS / 1e12, 4),
                     "unit": "T wave64-VALU-instructions/s", "frac": round(rate / VALU_PEAK_WAVE_INSTS, 4),
+                    "stream_ceiling": round(VALU_STREAM_CEILING / 1e12, 4),
+                    "frac_of_stream_ceiling": round(rate / VALU_STREAM_CEILING, 4),
                     "valu_insts_per_launch": round(meas["SQ_INSTS_VALU"]),
                     "valu_insts_per_ray": round(meas["SQ_INSTS_VALU"] * 64 / rays_per_launch, 1),
                     "source": src}
