@@ -436,7 +436,7 @@ def c_abi_multi(devices, floor, frames, steps, warmup, settle_s):
                 ms = wall / steps * 1e3
                 table[key] = {"ms_per_frame": round(ms, 4), "bit_identical": same}
                 if not same:
-                    raise SystemExit(f"c_abi_multi {fw}x{fh} {key}: frame differs from one GPU")
+                    raise RuntimeError(f"c_abi_multi {fw}x{fh} {key}: frame differs from one GPU")
                 if best is None or ms < best[1]:
                     best = (key, ms)
         out[f"{fw}x{fh}_{sname}"] = {
@@ -446,6 +446,41 @@ def c_abi_multi(devices, floor, frames, steps, warmup, settle_s):
         del bufs, want
     m.close()
     return out
+
+
+C_ABI_CHILD_TIMEOUT_S = 300
+
+
+def c_abi_multi_isolated(devices, steps, warmup, settle_s):
+    """c_abi_multi in a child process (bench.py --c-abi-child), so that a hang or a failure of
+    the single-process RCCL path costs its own line only, never the headline JSON line: the
+    child's result, or {"error": ...} on a non-zero exit, a bad frame or the time limit."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--c-abi-child", ",".join(map(str, devices)),
+           "--also-steps", str(steps), "--also-warmup", str(warmup), "--also-settle", str(settle_s)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=C_ABI_CHILD_TIMEOUT_S)
+    except subprocess.TimeoutExpired:
+        return {"devices": list(devices), "error": f"timed out after {C_ABI_CHILD_TIMEOUT_S} s"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        tail = (p.stderr or p.stdout).strip().splitlines()[-3:]
+        return {"devices": list(devices), "error": f"exit {p.returncode}: " + " | ".join(tail)}
+    return json.loads(lines[-1])
+
+
+def c_abi_child(devices_arg: str, steps: int, warmup: int, settle_s: float) -> None:
+    """bench.py --c-abi-child D0,D1,...: one c_abi_multi run, its result as one JSON line."""
+    devs = [int(d) for d in devices_arg.split(",") if d.strip()]
+    frames = [(7680, 4320, "lcg64")] + ([(16384, 16384, "lcg64")] if len(devs) >= 8 else [])
+    try:
+        out = c_abi_multi(devs, scenes.load_floor(), frames, steps, warmup, settle_s)
+    except RuntimeError as e:  # a frame that differs from the one-GPU frame
+        out = {"devices": devs, "error": str(e)}
+    print(json.dumps(out), flush=True)
 
 
 def main() -> None:
@@ -463,6 +498,7 @@ def main() -> None:
     ap.add_argument("--c-abi-devices", type=str, default="",
                     help="devices of the sfrt_multi line (default at N > 1: 0..N-1; e.g. 0,0,0,0 "
                          "rehearses it on one GPU with peer copies)")
+    ap.add_argument("--c-abi-child", type=str, default="", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the 8K / 16K frames")
     ap.add_argument("--headline-only", action="store_true",
@@ -473,6 +509,9 @@ def main() -> None:
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
+    if args.c_abi_child:
+        c_abi_child(args.c_abi_child, args.also_steps, args.also_warmup, args.also_settle)
+        return
     if os.environ.get("SFRT_RCCL_LIB"):
         raise SystemExit("bench.py measures real RCCL only; SFRT_RCCL_LIB names a test transport "
                          f"({os.environ['SFRT_RCCL_LIB']}): unset it")
@@ -594,9 +633,8 @@ def main() -> None:
     if c_devs and not (args.no_extra or args.headline_only):
         # the single-process multi-GPU path (C ABI), by rank 0 alone while the others wait
         if rank == 0:
-            frames = [(7680, 4320, "lcg64")] + ([(16384, 16384, "lcg64")] if len(c_devs) >= 8 else [])
-            result["also"]["c_abi_multi"] = c_abi_multi(c_devs, floor, frames, max(20, also_steps // 4),
-                                                        also_warmup, args.also_settle)
+            result["also"]["c_abi_multi"] = c_abi_multi_isolated(c_devs, max(20, also_steps // 4),
+                                                                 also_warmup, args.also_settle)
         if host_group is not None:
             dist.barrier(group=host_group)
     if world_size == 1 and not args.headline_only:
