@@ -26,7 +26,7 @@ namespace {
 __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; }
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
 __device__ __forceinline__ float gclamp(float x, float lo, float hi) { return gmin(gmax(x, lo), hi); }
-__device__ __forceinline__ float gmod(float x, float y) { return x - y * floorf(x / y); }
+// mod(x, y) = x - y * floor(x / y) (GLSL spec) is written out at its one use, :124-125.
 
 __device__ __forceinline__ float len3(float x, float y, float z) {
   return sqrt_cr((x * x + y * y) + z * z);
@@ -40,9 +40,9 @@ __device__ __forceinline__ void texel(const GlslFrame& f, int level, float s, fl
   const int i = fabsf(fu) < 16777216.0f ? ((int)fu & (w - 1)) : 0;  // w, h powers of two
   const int j = fabsf(fv) < 16777216.0f ? ((int)fv & (h - 1)) : 0;
   const uint32_t p = f.mip[f.mip_off[level] + j * w + i];
-  r = (float)(p & 255u) / 255.0f;
-  g = (float)((p >> 8) & 255u) / 255.0f;
-  b = (float)((p >> 16) & 255u) / 255.0f;
+  r = div255((float)(p & 255u));  // == / 255.0f (sfrt_device.h)
+  g = div255((float)((p >> 8) & 255u));
+  b = div255((float)((p >> 16) & 255u));
 }
 
 __device__ __forceinline__ uint32_t unorm8(float v) {
@@ -84,9 +84,10 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   float dz = (f.fwd[2] + f.right[2] * ax) + f.up[2] * ay;
   {
     const float l = len3(dx, dy, dz);                                     // :65
-    dx = dx / l;
-    dy = dy / l;
-    dz = dz / l;
+    const float a[3] = {dx, dy, dz};
+    float q[3];
+    div_shared(a, l, q);  // == dx / l, ... (one seed; sfrt_device.h)
+    dx = q[0]; dy = q[1]; dz = q[2];
   }
   const float cx = f.campos[0], cy = f.campos[1], cz = f.campos[2];
 
@@ -194,8 +195,23 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   const float rpy = sny * (1.0f - cw) + cw * (py - m.cy);
   const float rpz = snz * (1.0f - cw) + cw * (pz - m.cz);
   const float uv0 = m.uv[0];
-  const float ycoord = gmod(rpy / (0.8f + 0.2f * (fabsf(rpx) + fabsf(rpz))), uv0) + m.uv[3];
-  const float xcoord = gmod(gmin(fabsf(rpz), fabsf(rpx)), uv0) + m.uv[2];
+  // mod(v, uv0) = v - uv0 * floor(v / uv0) for both coordinates: the two divisions by uv0
+  // share a seed (div_shared), as do the lighting's divisions by tll and vl below
+  float yq;
+  {
+    const float a[1] = {rpy};
+    float q[1];
+    div_shared(a, 0.8f + 0.2f * (fabsf(rpx) + fabsf(rpz)), q);
+    yq = q[0];
+  }
+  const float xv = gmin(fabsf(rpz), fabsf(rpx));
+  float mq[2];
+  {
+    const float a[2] = {yq, xv};
+    div_shared(a, uv0, mq);
+  }
+  const float ycoord = (yq - uv0 * floorf(mq[0])) + m.uv[3];  // mod(yq, uv0) + uv.w
+  const float xcoord = (xv - uv0 * floorf(mq[1])) + m.uv[2];
   const float lod = total * 0.05f;
   float cr, cg, cbl;
   const int q = f.mip_levels - 1;
@@ -216,7 +232,13 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   }
 
   // ---- lighting (:128-151) ----
-  float bright = 1.0f / gmax(total, 1.0f);
+  float bright;
+  {
+    const float a[1] = {1.0f};
+    float q[1];
+    div_shared(a, gmax(total, 1.0f), q);
+    bright = q[0];
+  }
   const float lightc = ((float)draw < (float)f.sc ? 0.0f : 1.0f) *
                        ((float)(f.sc + f.lc - 1) < (float)draw ? 0.0f : 1.0f);
   const int nshadow = f.all - f.sc - f.lc;
@@ -224,10 +246,21 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
     const GlslBall L = ld(balls, li);
     const float tlx = L.x - px, tly = L.y - py, tlz = L.z - pz;
     const float tll = len3(tlx, tly, tlz);
-    const float tnx = tlx / tll, tny = tly / tll, tnz = tlz / tll;
+    // tl / tll (:133) and 10 / tll / tll (:150): four divisions by tll on one seed
+    float tq[4];
+    {
+      const float a[4] = {tlx, tly, tlz, 10.0f};
+      div_shared(a, tll, tq);
+    }
+    const float tnx = tq[0], tny = tq[1], tnz = tq[2];
     const float vx = rpx * nsign, vy = rpy * nsign, vz = rpz * nsign;
     const float vl = len3(vx, vy, vz);
-    const float nm = len3(vx / vl + tnx, vy / vl + tny, vz / vl + tnz) - 1.0f;
+    float vq[3];
+    {
+      const float a[3] = {vx, vy, vz};
+      div_shared(a, vl, vq);
+    }
+    const float nm = len3(vq[0] + tnx, vq[1] + tny, vq[2] + tnz) - 1.0f;
     float shadow = 1.0f;
     if (draw < f.sc + f.lc) {             // `drawSphere < j` holds for every j >= sc + lc
       const float t = gclamp((nm - 0.0f) / (0.5f - 0.0f), 0.0f, 1.0f);
@@ -246,7 +279,12 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
         shadow *= gclamp(sangle / P.sanglet + 1.0f - st * smooth_nm, 0.0f, 1.0f);
       }
     }
-    bright += 10.0f / tll / tll * gmax(0.5f + 0.5f * nm, 0.0f) * shadow;
+    float t2[1];  // (10 / tll) / tll
+    {
+      const float a[1] = {tq[3]};
+      div_shared(a, tll, t2);
+    }
+    bright += t2[0] * gmax(0.5f + 0.5f * nm, 0.0f) * shadow;
   }
 
   // ---- colour (:153-158) ----

@@ -113,6 +113,34 @@ __device__ __forceinline__ uint64_t ballot_bad_operand(float v) {
          __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(v) < 0x1.0p40f));
 }
 
+// a[i] / b for N numerators sharing one divisor, correctly rounded (the bits of `/`): one
+// reciprocal seed for all when every lane's operands lie in [2^-40, 2^40) (div_inrange's
+// domain, checked per compare: ballot_bad_operand); a wave with any other operand -- a zero
+// numerator among them -- divides plainly.
+template <int N>
+__device__ __forceinline__ void div_shared(const float (&a)[N], float b, float (&q)[N]) {
+  uint64_t bad = ballot_bad_operand(b);
+#pragma unroll
+  for (int i = 0; i < N; i++) bad |= ballot_bad_operand(a[i]);
+  if (bad == 0) {
+    const float y = div_seed(b);
+#pragma unroll
+    for (int i = 0; i < N; i++) q[i] = div_inrange(a[i], b, y);
+  } else {
+    const float bb = keep_branch(b);
+#pragma unroll
+    for (int i = 0; i < N; i++) q[i] = a[i] / bb;
+  }
+}
+
+// c / 255.0f for an integer c in [0, 255], correctly rounded: RN(c * RN(1/255)) corrected once
+// by Markstein's fma step (exact for all 256 c: tests/test_math_exhaustive.py::test_div255_exact, exact rationals).
+__device__ __forceinline__ float div255(float c) {
+  const float y = 0x1.010102p-8f;  // RN(1/255)
+  const float q = c * y;
+  return __builtin_fmaf(__builtin_fmaf(-255.0f, q, c), y, q);
+}
+
 // atan2f(y, x), bit for bit sfrt_math::atan2f (= glibc's e_atan2f.c), with a
 // cheaper path for the waves the renderers produce.  When every lane of the
 // wave has finite non-zero x and y and |y/x| in [2^-29, 2^25), no special case

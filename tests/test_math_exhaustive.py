@@ -29,3 +29,40 @@ def math_check(tmp_path_factory):
 def test_restated_math_matches_libm(math_check, args):
     r = subprocess.run([math_check] + args, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout + r.stderr
+
+
+def test_div255_exact():
+    """sfrt_device.h div255: q = RN(c * y), y = RN(1/255), then RN(q + RN(c - 255 q) * y) by two
+    fmas, equals the correctly rounded c / 255 for every integer c in [0, 255] (exact rationals;
+    the GLSL kernel's texel channels, rayShader.frag's texture() / 255)."""
+    from fractions import Fraction as Fr
+
+    import numpy as np
+
+    def rn(x: Fr) -> Fr:  # round to nearest binary32, ties to even (normal range)
+        if x == 0:
+            return Fr(0)
+        sign = -1 if x < 0 else 1
+        x = abs(x)
+        e = 0
+        while x >= 2:
+            x /= 2
+            e += 1
+        while x < 1:
+            x *= 2
+            e -= 1
+        m = x * 2 ** 23
+        fl = m.numerator // m.denominator
+        rem = m - fl
+        if rem > Fr(1, 2) or (rem == Fr(1, 2) and fl % 2 == 1):
+            fl += 1
+        return sign * Fr(fl) * Fr(2) ** (e - 23)
+
+    y = rn(Fr(1, 255))
+    assert y == Fr(float.fromhex("0x1.010102p-8"))
+    for c in range(256):
+        q = rn(c * y)
+        r = rn(c - 255 * q)  # fma(-255, q, c)
+        q2 = rn(q + r * y)   # fma(r, y, q)
+        assert q2 == rn(Fr(c, 255)), c
+        assert float(q2) == float(np.float32(np.float32(c) / np.float32(255))), c
