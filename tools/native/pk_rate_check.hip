@@ -2,7 +2,8 @@
 // shader clock while it runs (s_memtime against the 100 MHz s_memrealtime).  Eight waves per SIMD
 // (the sphere kernel's occupancy), sixteen independent chains per wave:
 //   mode 0: v_add_f32 + v_mul_f32 per chain; mode 1: the same element ops as v_pk_add_f32 +
-//   v_pk_mul_f32 on pairs; mode 2: v_add_f32 only.
+//   v_pk_mul_f32 on pairs; mode 2: v_add_f32 only; mode 3: v_add_f32 with an SGPR operand (one
+//   VGPR read per instruction instead of two).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -31,11 +32,18 @@ __global__ __launch_bounds__(256) void k(float* out, unsigned long long* clk, in
         __asm__ volatile("v_pk_add_f32 %0, %1, %0\n v_pk_mul_f32 %0, %1, %0" : "+v"(v) : "v"(a2));
         x[i] = v.x; x[i + 1] = v.y;
       }
-    } else {
+    } else if (MODE == 2) {
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         float v = x[i];
         __asm__ volatile("v_add_f32 %0, %1, %0\n v_add_f32 %0, %1, %0" : "+v"(v) : "v"(a));
+        x[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        float v = x[i];
+        __asm__ volatile("v_add_f32 %0, %1, %0\n v_add_f32 %0, %1, %0" : "+v"(v) : "s"(a));
         x[i] = v;
       }
     }
@@ -60,11 +68,12 @@ int main() {
   hipEventCreate(&e0); hipEventCreate(&e1);
   const int iters = 20000;
   for (int rep = 0; rep < 3; rep++)
-    for (int mode = 0; mode < 3; mode++) {
+    for (int mode = 0; mode < 4; mode++) {
       hipEventRecord(e0);
       if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(256), 0, 0, out, clk, iters, 1.0001f);
       if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(256), 0, 0, out, clk, iters, 1.0001f);
       if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(256), 0, 0, out, clk, iters, 1.0001f);
+      if (mode == 3) hipLaunchKernelGGL(k<3>, dim3(blocks), dim3(256), 0, 0, out, clk, iters, 1.0001f);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms = 0;
@@ -77,7 +86,8 @@ int main() {
       const double rate = waveinsts / ms / 1e9;
       printf("%-26s %.3f ms, %.1f T element-ops/s, %.3f T wave64-insts/s, s_memtime clock %.2f GHz,"
              " %.3f wave64-insts per SIMD-clock\n",
-             mode == 0 ? "v_add + v_mul" : mode == 1 ? "v_pk_add + v_pk_mul" : "v_add + v_add", ms,
+             mode == 0 ? "v_add + v_mul" : mode == 1 ? "v_pk_add + v_pk_mul"
+             : mode == 2 ? "v_add + v_add" : "v_add + v_add, SGPR operand", ms,
              elem_ops / ms / 1e9, rate, ghz, rate * 1e12 / (cus * 4.0 * ghz * 1e9));
     }
   return 0;
