@@ -205,3 +205,15 @@ def test_multi_create_without_gpu_fails_loudly(lib):
     h = ctypes.c_void_p()
     assert lib.sfrt_multi_create(devs, 2, sfrt.SFRT_MULTI_AUTO, ctypes.byref(h)) == -5
     assert lib.sfrt_multi_create(devs, 0, sfrt.SFRT_MULTI_AUTO, ctypes.byref(h)) == -1
+
+
+def test_bench_c_abi_line_failure_is_isolated():
+    """bench.py runs the single-process multi-GPU line in a child process: a child that fails
+    (here: no HIP device in this container) yields {"error": ...} for that line instead of
+    ending the parent, so the headline JSON line is never lost to it."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    out = bench.c_abi_multi_isolated([0, 1], 20, 5, 0.0)
+    assert out["devices"] == [0, 1]
+    assert "error" in out and "exit" in out["error"], out
