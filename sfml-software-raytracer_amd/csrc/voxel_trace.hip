@@ -47,8 +47,14 @@ __device__ __forceinline__ int16_t block_at(const VoxFrame& f, int32_t x, int32_
   if (key < 0) return kVoxEmpty;
   const int32_t cx = key >> 20, cy = (key >> 10) & 1023, cz = key & 1023;
   if (cx >= f.nx || cy >= f.ny || cz >= f.nz) return kVoxEmpty;
-  const long long c = ((long long)cx * f.ny + cy) * f.nz + cz;
-  return f.blocks[c];
+  // nx <= 2048, ny, nz <= 1024 (sfrt_voxel_set_blocks): the cell index is below 2^31 and every
+  // factor below 2^24, so 24-bit multiplies and a 32-bit byte offset are exact (the 64-bit
+  // index cost quarter-rate 64-bit multiplies at every DDA step)
+  uint32_t c;  // (cx * ny + cy) * nz + cz by two full-rate v_mad_u32_u24 (left alone, the
+               // compiler turns the first into a quarter-rate v_mad_u64_u32)
+  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"((uint32_t)cx), "s"((uint32_t)f.ny), "v"((uint32_t)cy));
+  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(c), "s"((uint32_t)f.nz), "v"((uint32_t)cz));
+  return *(const int16_t*)((const char*)f.blocks + c * 2u);
 }
 
 __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, uint32_t x,
