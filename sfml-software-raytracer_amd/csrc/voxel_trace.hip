@@ -287,9 +287,12 @@ __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
 // The default: 8x8 tiles on a 1-D grid of one-wave workgroups in the adaptive
 // tile order (sfrt_device.h sort_tiles; workgroup 0 is the sorter when
 // prev_cost is set).
-// Seven waves per SIMD: at most 72 VGPRs (the two raycast_t variants want 76, six
-// waves) with a 16-byte spill, measured 3% faster at 4K (profiles/ab/r2_ab15_voxel_waves.txt).
-__global__ __launch_bounds__(64, 7) void k_voxel_ordered(VoxFrame f, int tiles_x, int ntiles) {
+// Seven waves per SIMD: at most 72 VGPRs (71 since the 24-bit cell index, no spill; round 2
+// with a 16-byte spill measured 3% faster than six waves at 76, profiles/ab/r2_ab15_voxel_waves.txt).
+#ifndef SFRT_VOX_WAVES
+#define SFRT_VOX_WAVES 7
+#endif
+__global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f, int tiles_x, int ntiles) {
   const int lane = threadIdx.x & 63;
   int slot = (int)blockIdx.x;
   if (f.prev_cost) {
