@@ -35,6 +35,7 @@ whole 4K frame on the host cores, compared byte for byte with the GPU frame.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -47,10 +48,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+import bands as bands_mod  # noqa: E402
 import scenes  # noqa: E402
 import sfrt  # noqa: E402
-from bands import (BandPipeline, band_of, max_over_ranks as _max_over_ranks,  # noqa: E402,F401
-                   tune_spans)
+from bands import (BandPipeline, band_of, equal_spans,  # noqa: E402,F401
+                   max_over_ranks as _max_over_ranks, tune_spans)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # VALU issue peak: 256 CUs x 4 SIMD32 x one wave64 instruction per 2 clocks at
@@ -66,19 +68,19 @@ BYTES_PER_RAY = 4            # RGBA8 store; texture + sphere table are cache-res
 WIDTH, ROWS_PER_GPU = 3840, 2160
 
 
-def measured_traffic(pixels: int):
+def measured_traffic(pixels: int, kernel: str = "k_trace"):
     """Per-launch HBM bytes and VALU instruction counts of this workload from the
-    newest profiles/*_traffic.json (tools/rocprof_summary.py over separate
-    rocprofv3 --pmc passes of this same command), or None."""
+    newest profiles/*_traffic.json of `kernel` (tools/rocprof_summary.py over separate
+    rocprofv3 --pmc passes of this same workload), or None."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), reverse=True):
         doc = json.load(open(path))
-        if doc.get("kernel", "k_trace") != "k_trace":
+        if doc.get("kernel", "k_trace") != kernel:
             continue
         table = doc.get("per_launch_pixels", doc.get("per_grid_threads", {}))
-        # the steady-state launch has the tile-order sorter workgroup (+64 x R pixels, R = 4,
-        # 3, 2 or 1 pixels per lane)
-        for extra in (256, 192, 128, 64, 0):
+        # the sphere kernel's steady-state launch has the tile-order sorter workgroup (+64 x R
+        # pixels, R = 4, 3, 2 or 1 pixels per lane)
+        for extra in ((256, 192, 128, 64, 0) if kernel == "k_trace" else (0,)):
             ent = table.get(str(pixels + extra))
             if ent:
                 return ent, os.path.relpath(path, ROOT)
@@ -86,6 +88,32 @@ def measured_traffic(pixels: int):
 
 
 EVENT_EVERY = 8  # frames per HIP-event-timed frame in time_frames
+
+GOLDEN_PATH = os.path.join(ROOT, "tests", "golden", "golden.json")
+_GOLDEN = {}
+
+
+def golden_sha256(section: str, key):
+    """SHA-256 of a committed golden frame (tests/golden/golden.json, generated by
+    tests/golden/make_golden.py), or None.  Data, not the oracle: bench.py never runs it
+    outside cpu_baseline."""
+    if key is None:
+        return None
+    if not _GOLDEN:
+        _GOLDEN["doc"] = json.load(open(GOLDEN_PATH)) if os.path.exists(GOLDEN_PATH) else {}
+    return _GOLDEN["doc"].get(section, {}).get(key, {}).get("sha256")
+
+
+def verify_frame(frame, section: str, key) -> dict:
+    """A timed line's last frame against its golden frame: SHA-256 (hashlib) of the device
+    frame's bytes copied to the host.  {"golden": "section/key", "bit_identical": bool}, or
+    the digest alone where no golden frame exists for the workload."""
+    host = np.ascontiguousarray(frame.cpu().numpy()).reshape(-1)
+    digest = hashlib.sha256(host.data).hexdigest()
+    want = golden_sha256(section, key)
+    if want is None:
+        return {"golden": None, "sha256": digest}
+    return {"golden": f"{section}/{key}", "bit_identical": digest == want}
 
 
 def event_pair_ms(stream, n: int = 64) -> float:
@@ -218,10 +246,18 @@ def frame_row_costs(world, rank, world_size, height, pitch, stream, device="cuda
     return full[:height].cpu().numpy().astype(np.float32)
 
 
-def tuned_pipeline(world, rank, world_size, height, pitch, stream):
+def tuned_pipeline(world, rank, world_size, height, pitch, stream, band_mode="tuned"):
     """Row bands for this node: tune_spans times root-weighted and cost-weighted partitions,
     with RGBA8 and packed band transfers, on real frames (untimed warm-up) and keeps the
-    fastest; N = 1 is one whole band."""
+    fastest; N = 1 is one whole band.  band_mode "equal": the plain equal split (one gather
+    per frame), untuned."""
+    if band_mode == "equal" or world_size == 1:
+        spans = equal_spans(height, world_size)
+        pipe = BandPipeline(rank, world_size, height, pitch, "cuda", spans=spans)
+        return pipe, {"rows_per_rank": [n for _, n in spans], "root_factor": 1.0,
+                      "weights": "rows", "transfer": "rgba8",
+                      **({"tuning": "off (--bands equal)"} if world_size > 1 else {})}
+
     def render(band, row0, rows):
         world.render_band(band.data_ptr(), pitch, row0, rows, stream.cuda_stream)
     row_cost = frame_row_costs(world, rank, world_size, height, pitch, stream) \
@@ -289,21 +325,24 @@ def host_delivery(local_rank, floor, scene, width, height, frames, want):
 
 
 def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, stream,
-                  settle_s=0.0):
-    """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped transfer)."""
+                  settle_s=0.0, band_mode="tuned"):
+    """One extra BASELINE frame size, row-tiled over all ranks (+ overlapped transfer); rank 0
+    checks the last gathered frame against the golden frame of the workload."""
     world.set_scene(scene, width, height)
-    pipe, bands = tuned_pipeline(world, rank, world_size, height, width * 4, stream)
+    pipe, bands = tuned_pipeline(world, rank, world_size, height, width * 4, stream, band_mode)
     settle(world, width * 4, pipe.row0, pipe.rows, stream, settle_s)
     wall, kms = time_frames(world, pipe, width * 4, steps, warmup, stream)
     wall = max_over_ranks(wall)
     rays0 = width * pipe.rows
+    check = verify_frame(pipe.frame(steps - 1), "frames",
+                         scenes.golden_key(width, height, scene.name)) if rank == 0 else None
     del pipe
     return {"n_gpus": world_size, "Mrays_per_s": round(width * height * steps / wall / 1e6, 2),
             "fps": round(steps / wall, 2), "ms_per_frame": round(wall / steps * 1e3, 4),
             "kernel_ms_rank0_band": round(kms, 4),
             "hbm_frac_rank0_kernel": round(BYTES_PER_RAY * rays0 / (kms * 1e-3) / 1e9
                                            / HBM_PEAK_GBS, 6),
-            "bands": bands}
+            "bands": bands, **(check or {})}
 
 
 # BASELINE.json configs 4 and 5 (the 8K and 16384^2 frames also on one GPU: the
@@ -390,6 +429,11 @@ def c_abi_multi(devices, floor, frames, steps, warmup, settle_s):
     stream = torch.cuda.Stream(device=dev0)
     out = {"devices": list(devices),
            "transport": {sfrt.SFRT_MULTI_RCCL: "rccl", sfrt.SFRT_MULTI_PEER: "peer"}[m.transport]}
+    if m.transport == sfrt.SFRT_MULTI_RCCL:
+        # real RCCL only: a test transport is selected by an explicit call this script never makes
+        out["rccl_library"] = sfrt.multi_transport_library()
+        if out["rccl_library"].startswith("test:"):
+            raise RuntimeError(f"c_abi_multi: test transport {out['rccl_library']} in use")
     for fw, fh, sname in frames:
         scene = scenes.lcg64() if sname == "lcg64" else scenes.SCENES[sname]()
         m.set_scene(scene, fw, fh)
@@ -399,6 +443,8 @@ def c_abi_multi(devices, floor, frames, steps, warmup, settle_s):
             want = torch.empty(fh, fw * 4, dtype=torch.uint8, device=dev0)
             ref.render_band(want.data_ptr(), fw * 4, 0, fh, stream.cuda_stream)
             ref.check(stream.cuda_stream)
+        # every candidate's frame must equal `want`, and `want` the golden frame
+        want_check = verify_frame(want, "frames", scenes.golden_key(fw, fh, sname))
         bufs = [torch.empty(fh, fw * 4, dtype=torch.uint8, device=dev0) for _ in range(2)]
         table = {}
         best = None
@@ -442,7 +488,7 @@ def c_abi_multi(devices, floor, frames, steps, warmup, settle_s):
         out[f"{fw}x{fh}_{sname}"] = {
             "n_gpus": n, "Mrays_per_s": round(fw * fh / (best[1] * 1e-3) / 1e6, 2),
             "fps": round(1e3 / best[1], 2), "ms_per_frame": round(best[1], 4), "bands": best[0],
-            "candidates": table}
+            "candidates": table, **want_check}
         del bufs, want
     m.close()
     return out
@@ -483,6 +529,35 @@ def c_abi_child(devices_arg: str, steps: int, warmup: int, settle_s: float) -> N
     print(json.dumps(out), flush=True)
 
 
+class GlslBands:
+    """GlslShader.draw behind the render_band / check interface the timing helpers use
+    (rayShader.frag per render-target pixel)."""
+
+    def __init__(self, shader, width: int, height: int):
+        self.shader, self.width, self.height = shader, width, height
+
+    def render_band(self, dev_ptr, pitch, row0, rows, stream=0):
+        self.shader.draw(dev_ptr, self.width, self.height, pitch, row0, rows, stream)
+
+    def check(self, stream=0):
+        self.shader.check(stream)
+
+
+def valu_fraction(pixels: int, kernel: str, kernel_ms: float):
+    """The launch's VALU issue rate from the newest committed PMC pass of `kernel` at this
+    launch size (profiles/*_traffic.json) over this run's kernel time."""
+    meas, src = measured_traffic(pixels, kernel)
+    if not meas or "SQ_INSTS_VALU" not in meas or kernel_ms <= 0:
+        return None
+    rate = meas["SQ_INSTS_VALU"] / (kernel_ms * 1e-3)
+    out = {"frac": round(rate / VALU_PEAK_WAVE_INSTS, 4),
+           "frac_of_stream_ceiling": round(rate / VALU_STREAM_CEILING, 4),
+           "valu_insts_per_launch": round(meas["SQ_INSTS_VALU"]), "source": src}
+    if "hbm_bytes_per_launch" in meas:
+        out["traffic_bytes_per_launch"] = round(meas["hbm_bytes_per_launch"])
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -495,12 +570,21 @@ def main() -> None:
     ap.add_argument("--also-warmup", type=int, default=20, help="warm-up frames of those lines")
     ap.add_argument("--also-settle", type=float, default=0.2,
                     help="seconds of untimed frames before every line under also")
+    ap.add_argument("--bands", choices=("tuned", "equal"), default="tuned",
+                    help="N > 1 row bands: tuned during the warm-up (default) or the plain "
+                         "equal split, one gather per frame")
     ap.add_argument("--c-abi-devices", type=str, default="",
                     help="devices of the sfrt_multi line (default at N > 1: 0..N-1; e.g. 0,0,0,0 "
                          "rehearses it on one GPU with peer copies)")
     ap.add_argument("--c-abi-child", type=str, default="", help=argparse.SUPPRESS)
+    ap.add_argument("--rehearse", action="store_true",
+                    help="TEST ONLY, never a measurement: every rank on cuda:0 over a gloo "
+                         "process group (RCCL refuses two ranks on one device), point-to-point "
+                         "band transfers staged through host memory; runs the N > 1 body of "
+                         "this script on a one-GPU box (tests/test_bench_rehearsal.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the 8K / 16K frames")
+    ap.add_argument("--no-f1f2", action="store_true", help="skip the GLSL-mode and voxel lines")
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline workload (no also lines, no CPU baseline): the command "
                          "whose rocprof kernel trace profiles/*_kernel_stats_by_grid.csv summarises")
@@ -512,9 +596,6 @@ def main() -> None:
     if args.c_abi_child:
         c_abi_child(args.c_abi_child, args.also_steps, args.also_warmup, args.also_settle)
         return
-    if os.environ.get("SFRT_RCCL_LIB"):
-        raise SystemExit("bench.py measures real RCCL only; SFRT_RCCL_LIB names a test transport "
-                         f"({os.environ['SFRT_RCCL_LIB']}): unset it")
     if sfrt.build_flavour() != "release":
         raise SystemExit(f"bench.py measures the release library only; {sfrt.LIB_PATH} reports "
                          f"build flavour {sfrt.build_flavour()!r} (unset SFRT_LIB, rebuild)")
@@ -523,10 +604,15 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
-    torch.cuda.set_device(local_rank)
+    device = 0 if args.rehearse else local_rank
+    torch.cuda.set_device(device)
     host_group = None
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.rehearse:
+            dist.init_process_group("gloo")
+            bands_mod.stage_p2p_through_host()
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         # a host-side barrier for the c_abi_multi line: ranks waiting on an RCCL barrier
         # would keep a kernel spinning on the GPUs rank 0 renders on
         host_group = dist.new_group(backend="gloo")
@@ -539,12 +625,12 @@ def main() -> None:
     # RCCL gather (which orders itself after the current stream) all use it.
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    w = sfrt.World(local_rank)
+    w = sfrt.World(device)
     w.load_texture(*floor)
     w.set_scene(scene, WIDTH, height)
 
     settle(w, pitch, *band_of(rank, world_size, height), stream, args.settle)
-    pipe, bands = tuned_pipeline(w, rank, world_size, height, pitch, stream)
+    pipe, bands = tuned_pipeline(w, rank, world_size, height, pitch, stream, args.bands)
     row0, rows = pipe.row0, pipe.rows
     settle(w, pitch, row0, rows, stream, 0.1)  # the tuning's host work let the clock drop
     wall, kernel_ms = time_frames(w, pipe, pitch, args.steps, args.warmup, stream)
@@ -572,7 +658,8 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic: pinned 64-sphere cave (SURVEY 8d config 3), Floor.png texels",
             "config": {"workload": f"{WIDTH}x{height} lcg64 pose(0,0), {world_size} row band(s)"
-                                   + (" + RCCL transfer to rank 0 (overlapped, bands tuned)"
+                                   + (" + RCCL transfer to rank 0 (overlapped, bands "
+                                      + ("tuned)" if args.bands == "tuned" else "equal)")
                                       if world_size > 1 else ""),
                        "width": WIDTH, "height": height, "spheres": int(scene.spheres.shape[0]),
                        "camera": "static pose (0,0); moving-camera lines under also",
@@ -589,6 +676,13 @@ def main() -> None:
                                  "kernel time (HIP events on the launch stream around every 8th timed frame); the kernel is "
                                  "VALU-issue-bound, see valu_roofline and DESIGN.md"},
         }
+        if args.rehearse:
+            result["metric"] = "REHEARSAL, not a measurement: " + result["metric"]
+            result["rehearsal"] = {
+                "backend": "gloo" if world_size > 1 else None, "devices": "every rank on cuda:0",
+                "p2p": "staged through host memory (bands.stage_p2p_through_host)",
+                "note": "tests/test_bench_rehearsal.py: the N > 1 body of bench.py on a one-GPU "
+                        "box; the driver's SCALE run uses RCCL with one GPU per rank"}
         meas, src = measured_traffic(rays_per_launch)
         if meas:
             result["roofline"]["traffic"] = round(meas["hbm_bytes_per_launch"])
@@ -603,6 +697,9 @@ def main() -> None:
                     "valu_insts_per_launch": round(meas["SQ_INSTS_VALU"]),
                     "valu_insts_per_ray": round(meas["SQ_INSTS_VALU"] * 64 / rays_per_launch, 1),
                     "source": src}
+        # the last timed frame (gathered on rank 0 at N > 1) against the golden frame
+        result["frame_check"] = verify_frame(pipe.frame(args.steps - 1), "frames",
+                                             scenes.golden_key(WIDTH, height, "lcg64"))
     if world_size > 1 and rank == 0:
         # The last gathered frame must equal a single-GPU render of the whole frame.
         frame = pipe.frame(args.steps - 1)
@@ -618,7 +715,7 @@ def main() -> None:
         for fw, fh, sname in EXTRA_FRAMES.get(world_size, []):
             sc_x = scene if sname == "lcg64" else scenes.SCENES[sname]()
             line = measure_frame(w, sc_x, fw, fh, rank, world_size, also_steps, also_warmup,
-                                 stream, args.also_settle)
+                                 stream, args.also_settle, args.bands)
             if world_size == 1:  # one band: the kernel is the frame
                 line["hbm_frac"] = line.pop("hbm_frac_rank0_kernel")
                 line["kernel_ms"] = line.pop("kernel_ms_rank0_band")
@@ -628,8 +725,12 @@ def main() -> None:
         result["also"] = dict(extra)
         result["also_timing"] = {"steps": also_steps, "warmup": also_warmup,
                                  "settle_s": args.also_settle}
-    c_devs = [int(d) for d in args.c_abi_devices.split(",") if d.strip()] if args.c_abi_devices \
-        else (list(range(world_size)) if world_size > 1 else [])
+    if args.c_abi_devices:
+        c_devs = [int(d) for d in args.c_abi_devices.split(",") if d.strip()]
+    elif world_size > 1:
+        c_devs = [0] * world_size if args.rehearse else list(range(world_size))
+    else:
+        c_devs = []
     if c_devs and not (args.no_extra or args.headline_only):
         # the single-process multi-GPU path (C ABI), by rank 0 alone while the others wait
         if rank == 0:
@@ -638,8 +739,10 @@ def main() -> None:
         if host_group is not None:
             dist.barrier(group=host_group)
     if world_size == 1 and not args.headline_only:
-        def line(wx, fw, fh, name, per_frame=None, in_flight=1, **info):
-            """One N = 1 line under also: its own settle, warm-up and timed frames."""
+        def line(wx, fw, fh, name, per_frame=None, in_flight=1, golden=None, kernel="k_trace",
+                 **info):
+            """One N = 1 line under also: its own settle, warm-up and timed frames; its last
+            frame checked against golden = (section, key) of tests/golden/golden.json."""
             pipe_x = BandPipeline(0, 1, fh, fw * 4, "cuda", local_depth=in_flight)
             settle(wx, fw * 4, 0, fh, stream, args.also_settle)
             wall_x, k_x = time_frames(wx, pipe_x, fw * 4, also_steps, also_warmup, stream,
@@ -649,63 +752,97 @@ def main() -> None:
                    "ms_per_frame": round(wall_x / also_steps * 1e3, 4)}
             if in_flight == 1:
                 rec.update(kernel_ms=round(k_x, 4), hbm_frac=hbm_frac(fw * fh, k_x))
+                if kernel != "k_trace":
+                    rec["valu"] = valu_fraction(fw * fh, kernel, k_x)
             else:
                 rec.update(kernel_ms_per_launch_overlapping=round(k_x, 4), frames_in_flight=in_flight,
                            streams=in_flight)
             rec.update(info)
+            rec.update(verify_frame(pipe_x.frame(also_steps - 1), *(golden or ("frames", None))))
             result["also"][name] = rec
             del pipe_x
 
         # BASELINE config 2: 1920x1080, 10-sphere scene.
-        w2 = sfrt.World(local_rank)
+        w2 = sfrt.World(device)
         w2.load_texture(*floor)
         w2.set_scene(scenes.default10(), 1920, 1080)
-        line(w2, 1920, 1080, "1920x1080_default10")
+        line(w2, 1920, 1080, "1920x1080_default10",
+             golden=("frames", scenes.golden_key(1920, 1080, "default10")))
         w2.close()
         # BASELINE config 3 with "all textures": every reference texture resident, one
         # per sphere (the per-sphere texture extension; the main line is textures[0]).
-        w3 = sfrt.World(local_rank)
+        w3 = sfrt.World(device)
         for slot, (rgba, tw, th) in enumerate(scenes.load_all_textures()):
             w3.load_texture(rgba, tw, th, slot=slot)
         w3.set_scene(scene, WIDTH, height)
         w3.set_sphere_textures(scenes.all_texture_slots(scene.spheres.shape[0]))
-        line(w3, WIDTH, height, "3840x2160_lcg64_all_textures")
+        line(w3, WIDTH, height, "3840x2160_lcg64_all_textures",
+             golden=("all_textures", f"{WIDTH}x{height}_lcg64@0,0"))
         w3.close()
         # The adaptive tile order dispatches each frame's tiles longest-first
         # by recorded march steps.  The same workload with a camera turning every frame, in
         # both orders, and the static camera in plain row-major order.  Only the camera
-        # changes per frame (one C-ABI call).
+        # changes per frame (one C-ABI call).  The turn ends at pose (0, 0) on the last timed
+        # frame, so that frame is checked against the headline's golden frame.
+        last = also_warmup + also_steps - 1
+        key4k = ("frames", scenes.golden_key(WIDTH, height, "lcg64"))
 
         def turn(k):
-            w.set_camera(scene.cam_pos, 0.004 * k, 0.0)
+            w.set_camera(scene.cam_pos, 0.004 * (k - last), 0.0)
         for order, key in ((1, "3840x2160_lcg64_turning"), (0, "3840x2160_lcg64_turning_row_major"),
                            (0, "3840x2160_lcg64_row_major")):
             w.set_scene(scene, WIDTH, height)
             w.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
             moving = "turning" in key
-            line(w, WIDTH, height, key, per_frame=turn if moving else None,
-                 camera="rotation = 0.004 rad x frame index" if moving else "static pose (0,0)",
+            line(w, WIDTH, height, key, per_frame=turn if moving else None, golden=key4k,
+                 camera="rotation = 0.004 rad x (frame index - last frame's)" if moving
+                 else "static pose (0,0)",
                  tile_order="adaptive" if order else "row-major (SFRT_OPT_TILE_ORDER 0)")
         w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
         w.set_scene(scene, WIDTH, height)
         # Beyond the reference's scene sizes: 256 spheres (the n > 64 kernel).
-        w5 = sfrt.World(local_rank)
+        w5 = sfrt.World(device)
         w5.load_texture(*floor)
         w5.set_scene(scenes.lcg256(), WIDTH, height)
-        line(w5, WIDTH, height, "3840x2160_lcg256", spheres=256)
+        line(w5, WIDTH, height, "3840x2160_lcg256", spheres=256,
+             golden=("frames", scenes.golden_key(WIDTH, height, "lcg256")))
         w5.close()
         # Two frames in flight (see frame_streams): the 4K static and 1080p frames.
         for key, (fw, fh, sc2) in (("3840x2160_lcg64_2_in_flight", (WIDTH, height, scene)),
                                    ("1920x1080_default10_2_in_flight", (1920, 1080, scenes.default10()))):
-            w6 = sfrt.World(local_rank)
+            w6 = sfrt.World(device)
             w6.load_texture(*floor)
             w6.set_scene(sc2, fw, fh)
-            line(w6, fw, fh, key, in_flight=2)
+            line(w6, fw, fh, key, in_flight=2, golden=("frames", scenes.golden_key(fw, fh, sc2.name)))
             w6.close()
+        if not args.no_f1f2:
+            # SURVEY 8f rows f1 (GLSL mode, rayShader.frag:63-161) and f2 (voxel World,
+            # World.cpp:302-491) under the same rules: settle, warm-up, timed frames, kernel
+            # time from HIP events on the launch stream, the last frame against its golden.
+            import glsl_scenes
+            import voxel_scenes
+            sh = sfrt.GlslShader(device)
+            sh.set_ground(*floor)
+            for fw, fh in ((1920, 1080), (WIDTH, height)):
+                sh.set_uniforms(glsl_scenes.default_uniforms(fw, fh))
+                line(GlslBands(sh, fw, fh), fw, fh, f"glsl_{fw}x{fh}", kernel="k_glsl",
+                     golden=("glsl", f"default@{fw}x{fh}"),
+                     scene="constructor scene (srand 0), rot (0,0)", unit="fragments")
+            sh.close()
+            vw = sfrt.VoxelWorld(device)
+            vtex, vdyn = voxel_scenes.load_textures()
+            vw.load_assets(vtex, vdyn, voxel_scenes.COLORS)
+            pos = (15.5, 1.9, 15.5)
+            for fw, fh in ((1920, 1080), (WIDTH, height)):
+                vw.set_scene(voxel_scenes.default_world(pos, 0.0, 0.0), fw, fh)
+                line(vw, fw, fh, f"voxel_{fw}x{fh}", kernel="k_voxel",
+                     golden=("voxel", f"{fw}x{fh}@{pos[0]:g},{pos[1]:g},{pos[2]:g}/0,0"),
+                     scene="default world, pose (15.5,1.9,15.5)/(0,0)")
+            vw.close()
         torch.cuda.synchronize()
         gpu_frame = pipe.frame(args.steps - 1).cpu().numpy().ravel()
         result["also"]["3840x2160_lcg64_to_host"] = dict(
-            host_delivery(local_rank, floor, scene, WIDTH, height, 200, gpu_frame),
+            host_delivery(device, floor, scene, WIDTH, height, 200, gpu_frame),
             note="PCIe-inclusive (frame copied into a host buffer), not the HBM-resident value")
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(scene, WIDTH, height, floor, gpu_frame)

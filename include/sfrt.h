@@ -224,6 +224,16 @@ typedef struct sfrt_multi sfrt_multi;
 #define SFRT_MULTI_PEER 2
 
 SFRT_API int sfrt_multi_create(const int* hip_devices, int n, int transport, sfrt_multi** out);
+/* The library behind SFRT_MULTI_RCCL: "" until the process's first RCCL context, then
+ * "librccl.so.1" (or "librccl.so"), or "test:<path>" for a test transport; " (not loaded)"
+ * is appended when it did not resolve.  SFRT_E_INVALID if it does not fit in `size`. */
+SFRT_API int sfrt_multi_transport_library(char* buf, int size);
+/* TEST ONLY: the RCCL C API from `library_path` instead of librccl (the tests' loopback
+ * transport, tests/native/rccl_loopback.cpp, which accepts a device listed twice, so the
+ * RCCL branch runs with n > 1 on one GPU).  Only before the process's first RCCL context
+ * (else SFRT_E_INVALID); nothing in the environment selects it; reported by
+ * sfrt_multi_transport_library. */
+SFRT_API int sfrt_multi_use_test_transport(const char* library_path);
 SFRT_API void sfrt_multi_destroy(sfrt_multi* m);
 SFRT_API int sfrt_multi_count(const sfrt_multi* m, int* n, int* transport);
 SFRT_API int sfrt_multi_world(sfrt_multi* m, int rank, sfrt_world** out);

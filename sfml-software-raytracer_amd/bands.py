@@ -115,6 +115,55 @@ def check_spans(spans, height: int) -> None:
         raise ValueError(f"bands {spans} do not tile {height} rows")
 
 
+class _HostStagedWork:
+    """A point-to-point transfer staged through host memory (see stage_p2p_through_host).
+    wait() blocks on the host transfer, then a receive copies into its device tensor on the
+    caller's current stream -- the stream-side order NCCL's Work.wait() gives: work queued on
+    that stream afterwards sees the bytes."""
+
+    def __init__(self, work, host, dst=None):
+        self.work, self.host, self.dst = work, host, dst
+
+    def wait(self):
+        if self.work is None:
+            return
+        self.work.wait()
+        self.work = None
+        if self.dst is not None:
+            self.dst.copy_(self.host)
+            self.dst = None
+
+
+def _host_staged_batch_isend_irecv(ops):
+    works = []
+    for op in ops:
+        if op.op is dist.isend:
+            host = op.tensor.to("cpu")  # waits for the current stream's work (the render)
+            works.append(_HostStagedWork(dist.isend(host, op.peer, tag=op.tag), host))
+        else:
+            host = torch.empty(op.tensor.shape, dtype=op.tensor.dtype)
+            works.append(_HostStagedWork(dist.irecv(host, op.peer, tag=op.tag), host, op.tensor))
+    return works
+
+
+_P2P = {"staged": False}
+
+
+def stage_p2p_through_host(on: bool = True) -> None:
+    """TEST ONLY (bench.py --rehearse): BandPipeline's point-to-point transfers of device
+    bands go through host copies, for a gloo process group whose ranks share one GPU (RCCL
+    refuses two ranks on one device, and gloo's send/recv take host buffers).  The gather of
+    equal bands and the all-reduces keep their device tensors (gloo's HIP paths)."""
+    _P2P["staged"] = bool(on)
+
+
+def batch_isend_irecv(ops):
+    """dist.batch_isend_irecv, or its host-staged stand-in after stage_p2p_through_host()."""
+    if _P2P["staged"]:
+        return _host_staged_batch_isend_irecv(ops)
+    return dist.batch_isend_irecv(ops)
+
+
 class BandPipeline:
     """Row-band frames with the transfer to rank 0 overlapped with rendering.
 
@@ -211,9 +260,9 @@ class BandPipeline:
         elif self.rank == 0:
             ops = [dist.P2POp(dist.irecv, views[r], r) for r in range(1, self.world_size)
                    if self.spans[r][1] > 0]
-            self.pending[b] = dist.batch_isend_irecv(ops) if ops else []
+            self.pending[b] = batch_isend_irecv(ops) if ops else []
         elif self.rows > 0:
-            self.pending[b] = dist.batch_isend_irecv([dist.P2POp(dist.isend, band, 0)])
+            self.pending[b] = batch_isend_irecv([dist.P2POp(dist.isend, band, 0)])
 
     def _submit_packed(self, b: int, band, views) -> None:
         sf = self._sfrt
@@ -221,13 +270,13 @@ class BandPipeline:
             if self.rows > 0:
                 sf.band_pack(band.data_ptr(), self.pixels[self.rank], self.packbuf[b].data_ptr(),
                              torch.cuda.current_stream().cuda_stream)
-                self.pending[b] = dist.batch_isend_irecv(
+                self.pending[b] = batch_isend_irecv(
                     [dist.P2POp(dist.isend, self.packbuf[b], 0)])
             return
         srcs = [r for r in range(1, self.world_size) if self.pixels[r]]
         if not srcs:
             return
-        works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.stage[b][r], r) for r in srcs])
+        works = batch_isend_irecv([dist.P2POp(dist.irecv, self.stage[b][r], r) for r in srcs])
         with torch.cuda.stream(self.unpack_stream):
             for work in works:
                 work.wait()  # the unpack stream waits for the receives

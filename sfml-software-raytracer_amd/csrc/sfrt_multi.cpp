@@ -18,9 +18,11 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "sfrt.h"
@@ -30,10 +32,12 @@ namespace {
 
 // RCCL entry points, resolved from librccl.so.1 by the first RCCL context (a
 // process that already loaded RCCL -- e.g. torch's copy -- gets that one), so
-// the single-GPU library carries no RCCL dependency.  SFRT_RCCL_LIB names another
-// library with the same C API instead: the tests' loopback transport
-// (tests/native/rccl_loopback.cpp), which -- unlike RCCL -- accepts a device listed
-// twice, so the RCCL branch below runs with n > 1 on a one-GPU box.
+// the single-GPU library carries no RCCL dependency.  A test may name another library
+// with the same C API instead, explicitly and before that first context
+// (sfrt_multi_use_test_transport: the tests' loopback transport,
+// tests/native/rccl_loopback.cpp, which -- unlike RCCL -- accepts a device listed twice, so
+// the RCCL branch below runs with n > 1 on a one-GPU box).  Nothing in the environment
+// selects it, and sfrt_multi_transport_library reports which library is in use.
 struct Rccl {
   decltype(&ncclCommInitAll) comm_init_all = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
@@ -43,21 +47,36 @@ struct Rccl {
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   bool ok = false;
-  bool override_lib = false;  // SFRT_RCCL_LIB: not librccl
+  bool override_lib = false;  // a test transport, not librccl
+  std::string name;           // the library the entry points came from
 };
+
+std::mutex g_rccl_mu;
+std::string g_test_transport;  // sfrt_multi_use_test_transport
+bool g_rccl_resolved = false;
 
 const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
+    std::string alt;
+    {
+      std::lock_guard<std::mutex> lk(g_rccl_mu);
+      alt = g_test_transport;
+      g_rccl_resolved = true;
+    }
     void* h = nullptr;
-    const char* alt = getenv("SFRT_RCCL_LIB");
-    if (alt && *alt) {
-      h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+    if (!alt.empty()) {
+      h = dlopen(alt.c_str(), RTLD_NOW | RTLD_LOCAL);
       r.override_lib = true;
+      r.name = alt;
     } else {
+      r.name = "librccl.so.1";
       h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-      if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) {
+        r.name = "librccl.so";
+        h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+      }
     }
     if (!h) return;
     r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
@@ -438,6 +457,30 @@ struct sfrt_multi {
 
 extern "C" {
 
+int sfrt_multi_use_test_transport(const char* library_path) {
+  if (!library_path || !*library_path) return SFRT_E_INVALID;
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  if (g_rccl_resolved) return SFRT_E_INVALID;  // the process already resolved its transport
+  g_test_transport = library_path;
+  return SFRT_OK;
+}
+
+int sfrt_multi_transport_library(char* buf, int size) {
+  if (!buf || size <= 0) return SFRT_E_INVALID;
+  bool resolved;
+  {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    resolved = g_rccl_resolved;
+  }
+  std::string name;
+  if (resolved) {
+    const Rccl& r = rccl();
+    name = (r.override_lib ? "test:" : "") + r.name + (r.ok ? "" : " (not loaded)");
+  }
+  std::snprintf(buf, (size_t)size, "%s", name.c_str());
+  return (int)name.size() < size ? SFRT_OK : SFRT_E_INVALID;
+}
+
 int sfrt_multi_create(const int* hip_devices, int n, int transport, sfrt_multi** out) {
   if (!out) return SFRT_E_INVALID;
   *out = nullptr;
@@ -451,7 +494,7 @@ int sfrt_multi_create(const int* hip_devices, int n, int transport, sfrt_multi**
     for (int q = 0; q < r; q++) distinct = distinct && hip_devices[q] != hip_devices[r];
   }
   if (transport == SFRT_MULTI_AUTO) transport = distinct ? SFRT_MULTI_RCCL : SFRT_MULTI_PEER;
-  // RCCL refuses a device listed twice (the SFRT_RCCL_LIB loopback does not)
+  // RCCL refuses a device listed twice (the tests' loopback transport does not)
   if (transport == SFRT_MULTI_RCCL && (!rccl().ok || (!distinct && !rccl().override_lib)))
     return SFRT_E_INVALID;
   sfrt_multi* m = new sfrt_multi();

@@ -90,10 +90,13 @@ struct PixelDump {
 
 // Float intermediates out of the frame-fill kernels themselves (sfrt_world_trace_points):
 // the DUMP instantiation of the same march and shading, plus an epilogue that writes
-// pixel (a, b)'s record to out[index[(b - sub_row0) * sub_w + a]] when that is >= 0.
+// pixel (a, b)'s record to out[q] when pix[q] == (b - sub_row0) * sub_w + a (binary search
+// of the sorted, distinct listed pixels: O(listed pixels) memory whatever the frame size).
+// The DUMP kernels store no frame pixel (each record carries its rgba).
 struct DumpArgs {
-  const int32_t* index;  // sub_rows x sub_w, -1 = no record
-  PixelDump* out;
+  const int64_t* pix;  // ascending, distinct
+  int npix;
+  PixelDump* out;      // npix records
 };
 
 // sphere_trace.hip.  dump != nullptr: the DUMP instantiation of the kernel the table picks.

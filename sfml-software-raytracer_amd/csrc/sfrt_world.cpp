@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstring>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "sfrt.h"
@@ -131,6 +132,7 @@ struct sfrt_world {
   size_t d_tex_texels = 0;
   int* d_status = nullptr;
   sfrt::TileChains scheds;  // adaptive tile order (sfrt_sched.h), one chain per stream
+  sfrt::TileSched dump_sched;  // sfrt_world_trace_points' own chain (never the frames')
   int cur_chain = 0;        // the chain of the launch between sched_begin and sched_end
   // Device copies of the sphere records for launches that read them from memory
   // (> 64 spheres, trace_points): a ring of slots, each with pinned staging and
@@ -176,6 +178,7 @@ struct sfrt_world {
     }
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     scheds.release();
+    dump_sched.release();
     (void)hipFree(d_tex);
     (void)hipFree(d_status);
     (void)hipDeviceSynchronize();
@@ -763,32 +766,37 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
   // The listed pixels come out of the frame-fill kernel itself (its DUMP instantiation,
   // sphere_trace.hip): a whole frame with the world's options -- the kernel table's tile
   // shape or SFRT_OPT_RAYS_PER_LANE, culling -- in the adaptive tile order when that is
-  // on (three launches on the world's stream, so the last one runs in a sorted order),
-  // row-major otherwise.  index: pixel -> first listed position (repeats copied below).
-  const size_t px = (size_t)w->width * w->height;
-  std::vector<int32_t> index(px, -1);
-  for (int k = 0; k < count; k++) {
-    int32_t& q = index[(size_t)ij[2 * k + 1] * w->width + ij[2 * k]];
-    if (q < 0) q = k;
+  // on (three launches, so the last one runs in a sorted order), row-major otherwise.
+  // Memory is O(count): the kernel binary-searches the sorted distinct pixel ids and
+  // stores no frame.  The launches run on a private tile-order chain (dump_sched), so
+  // the world's own chains, its last fill (sfrt_world_row_costs) and the next frame's
+  // order are those of the caller's last render, untouched by the dump.
+  std::vector<std::pair<int64_t, int>> ids((size_t)count);
+  for (int k = 0; k < count; k++)
+    ids[k] = {(int64_t)ij[2 * k + 1] * w->width + ij[2 * k], k};
+  std::sort(ids.begin(), ids.end());
+  std::vector<int64_t> pix;
+  std::vector<int> slot((size_t)count);  // listed position -> distinct entry
+  for (const auto& e : ids) {
+    if (pix.empty() || pix.back() != e.first) pix.push_back(e.first);
+    slot[e.second] = (int)pix.size() - 1;
   }
   sfrt::DeviceGuard g(w->device);
-  if (w->d_frame_px < px) {
-    (void)hipFree(w->d_frame);
-    w->d_frame = nullptr;
-    w->d_frame_px = 0;
-    HIP_TRY(hipMalloc(&w->d_frame, px * 4));
-    w->d_frame_px = px;
-  }
   sfrt::DumpArgs dump{};
-  if (hipMalloc((void**)&dump.index, sizeof(int32_t) * px) != hipSuccess ||
-      hipMalloc(&dump.out, sizeof(sfrt::PixelDump) * (size_t)count) != hipSuccess) {
-    (void)hipFree((void*)dump.index);
+  dump.npix = (int)pix.size();
+  std::vector<sfrt::PixelDump> got(pix.size());
+  int64_t* d_pix = nullptr;
+  if (hipMalloc((void**)&d_pix, sizeof(int64_t) * pix.size()) != hipSuccess ||
+      hipMalloc(&dump.out, sizeof(sfrt::PixelDump) * pix.size()) != hipSuccess) {
+    (void)hipFree(d_pix);
     return SFRT_E_HIP;
   }
+  dump.pix = d_pix;
   auto run = [&]() -> int {
-    HIP_TRY(hipMemcpyAsync((void*)dump.index, index.data(), sizeof(int32_t) * px,
-                           hipMemcpyHostToDevice, w->stream));
+    HIP_TRY(hipMemcpyAsync(d_pix, pix.data(), sizeof(int64_t) * pix.size(), hipMemcpyHostToDevice,
+                           w->stream));
     const int passes = w->tile_order_on ? 3 : 1;
+    w->dump_sched.reset();  // this frame's own order: record, sort, use
     for (int q = 0; q < passes; q++) {
       sfrt::FrameRec f;
       std::vector<sfrt::SphereRec> recs;
@@ -798,33 +806,35 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
       f.sub_row0 = 0;
       f.sub_rows = w->height;
       f.tiles_x = (w->width + sfrt::kTile - 1) / sfrt::kTile;
-      f.out = w->d_frame;
+      f.out = nullptr;  // the DUMP kernels store records only
       f.out_pitch = w->width;
       int rc2 = w->stage_spheres(f, recs, w->stream, false);
       if (rc2) return rc2;
+      sfrt::TileSchedPtrs p;
       if (w->tile_order_on) {
-        if ((rc2 = w->sched_begin(f, w->stream))) return rc2;
-        if ((rc2 = w->sched_end(f, w->stream,
-                                sfrt::launch_trace(f, recs.data(), w->stream, &dump) == 0)))
-          return rc2;
-      } else if (sfrt::launch_trace(f, recs.data(), w->stream, &dump)) {
-        return SFRT_E_HIP;
+        long long tiles = 0;
+        const long long key = sfrt::trace_tile_key(f, &tiles);
+        HIP_TRY(w->dump_sched.begin(key, tiles, w->stream, w->tile_order_on, p));
+        f.tile_order = p.tile_order;
+        f.tile_cost = p.tile_cost;
+        f.prev_cost = p.prev_cost;
+        f.next_order = p.next_order;
       }
+      const bool queued = sfrt::launch_trace(f, recs.data(), w->stream, &dump) == 0;
+      if (w->tile_order_on) HIP_TRY(w->dump_sched.end(p, w->stream, queued));
+      if (!queued) return SFRT_E_HIP;
       if ((rc2 = w->launched(w->stream))) return rc2;
     }
-    HIP_TRY(hipMemcpyAsync(out, dump.out, sizeof(sfrt::PixelDump) * (size_t)count,
+    HIP_TRY(hipMemcpyAsync(got.data(), dump.out, sizeof(sfrt::PixelDump) * pix.size(),
                            hipMemcpyDeviceToHost, w->stream));
     return SFRT_OK;
   };
   rc = run();
   const int st = w->read_status(w->stream);
-  (void)hipFree((void*)dump.index);
+  (void)hipFree(d_pix);
   (void)hipFree(dump.out);
   if (rc || st) return rc ? rc : st;
-  for (int k = 0; k < count; k++) {
-    const int32_t q = index[(size_t)ij[2 * k + 1] * w->width + ij[2 * k]];
-    if (q != k) out[k] = out[q];
-  }
+  for (int k = 0; k < count; k++) std::memcpy(&out[k], &got[slot[k]], sizeof(sfrt_pixel_dump));
   return SFRT_OK;
 }
 

@@ -23,19 +23,14 @@
 
 #include "sfrt_device.h"
 #include "sfrt_math.h"
+#include "sfrt_probe.h"
 #include "sfrt_trace.h"
 
 #pragma clang fp contract(off)
 
-// Diagnostic builds only (tools/ab_libs.py, tools/tile_timeline.py), never the shipped
-// library: -DSFRT_EXP=16 writes per-tile wall-clock start/end into each tile's first
-// pixels, -DSFRT_EXP=32 per-tile march counters (steps, sphere visits, visits that
-// passed for some ray, window/slot mode, culled spheres; tools/visit_counts.py),
-// -DSFRT_EXP=64 skips the shading tail, 128 / 256 replace its atan2f / asinf by a multiply
-// (timing probes; all write wrong bytes).
-#ifndef SFRT_EXP
-#define SFRT_EXP 0
-#endif
+// Diagnostic builds (-DSFRT_EXP=<bits>: timing and counter probes that write wrong bytes) go
+// through the probe type P of trace_tile_window_r (sfrt_probe.h); the shipped library's
+// NoProbe hooks are empty.
 #ifndef SFRT_BUILD_FLAVOUR
 #define SFRT_BUILD_FLAVOUR "release"
 #endif
@@ -83,13 +78,10 @@ struct Shading {
   bool outside;
 };
 
+template <class P>
 __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRec& d, float px,
                                                float py, float pz, PixelDump* dump) {
-#if SFRT_EXP & 128  // timing probe only (wrong bytes): the atan2f call replaced by one multiply
-  float ang = d.atan_c - pz * px;
-#else
-  float ang = d.atan_c - atan2f_wave(pz, px);  // == sfrt_math::atan2f (sfrt_device.h)
-#endif
+  float ang = d.atan_c - P::hit_atan2(pz, px);  // atan2f_wave == sfrt_math::atan2f (sfrt_device.h)
   ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
   const float xcoord = sfrt_math::div_pi2_plus_1(ang);  // == ang / PI2 + 1.0f
   const float ex = px - d.cx, ey = py - d.cy, ez = pz - d.cz;
@@ -107,11 +99,7 @@ __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRe
     ny = ey / keep_branch(el);
     brightness = 3.0f / keep_branch(bd);
   }
-#if SFRT_EXP & 256  // timing probe only (wrong bytes): the asinf call replaced by a multiply
-  const float ycoord = sfrt_math::div_pi_plus_half(ny * 0.7f);
-#else
-  const float ycoord = sfrt_math::div_pi_plus_half(sfrt_math::asinf(ny));  // == asinf / PI + 0.5f
-#endif
+  const float ycoord = sfrt_math::div_pi_plus_half(P::hit_asin(ny));  // == asinf / PI + 0.5f
   // fmodf(v, 1.0f) == v - truncf(v) exactly for every binary32 v (NaN/inf -> NaN).
   // texsize of textures[0] (or of the sphere's extension slot), (float)(unsigned) as :376
   const uint32_t tw = d.tex_wh & 0xffffu, th = d.tex_wh >> 16;
@@ -139,7 +127,7 @@ __device__ __forceinline__ Shading shade_texel(const FrameRec& f, const SphereRe
 }
 
 // (Uint8)(component * brightness) for r, g, b; alpha kept (:377-379, :109).
-__device__ __forceinline__ uint32_t shade_rgba(uint32_t texel, float brightness) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t shade_rgba(uint32_t texel, float brightness) {
   const uint32_t r = __float2uint_rz((float)(texel & 0xffu) * brightness);
   const uint32_t g = __float2uint_rz((float)((texel >> 8) & 0xffu) * brightness);
   const uint32_t b = __float2uint_rz((float)((texel >> 16) & 0xffu) * brightness);
@@ -415,14 +403,14 @@ __device__ __forceinline__ bool pass_body_r(const float (&ss)[R], float s_pass, 
 // it is, which keeps the tile cone tight.
 // DUMP (sfrt_world_trace_points only): the same march and shading, plus a per-ray
 // iteration count and an epilogue writing the float intermediates of listed pixels.
-template <int R, bool LIST, bool DUMP>
+// P: the probe hooks (sfrt_probe.h; NoProbe in the shipped library, all empty).
+template <int R, bool LIST, bool DUMP, class P>
 __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
                                                     const SphereRec* __restrict__ sph,
                                                     DumpArgs dmp) {
   const int lane = threadIdx.x & 63;
-#if SFRT_EXP & 512  // with 16: the wave's entry time in place of its slot (wrong bytes)
-  const uint64_t dbg_entry = __builtin_amdgcn_s_memrealtime();
-#endif
+  P probe;
+  probe.wave_entry();
   // Adaptive tile order (sfrt_trace.h FrameRec): workgroup 0 may be the sorter.
   const int ntiles = f.tiles_x * ((f.sub_rows + kTile - 1) / kTile);
   int slot = (int)blockIdx.x;
@@ -441,12 +429,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   const int tile_y = tile / f.tiles_x;  // f.tiles_x = ceil(sub_w / (8 R)) for this kernel
   const int tile_x = tile - tile_y * f.tiles_x;
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
-#if SFRT_EXP & 16  // diagnostic build: per-tile wall-clock start/end (wrong bytes)
-  const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
-#if SFRT_EXP & 1024  // and the tile's shader clocks (s_memtime) in place of its trips
-  const uint64_t dbg_c0 = __builtin_amdgcn_s_memtime();
-#endif
-#endif
+  probe.tile_begin();
   const int b = f.sub_row0 + tile_y * kTile + (lane >> 3);
   const int b_end = f.sub_row0 + f.sub_rows;
   const int bc = b < b_end ? b : b_end - 1;
@@ -525,6 +508,10 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   // First set bit of a 64-bit culling mask, 63 for an empty mask (s_ff1 gives -1): entry 63 is
   // always readable -- a record of the n <= 64 kernel's argument block, or lane 63 of the list
   // (its sphere, or sphere 63 < n) -- so a lookahead past the last entry loads a record it never uses.
+  static_assert(kInlineSpheres == 64,
+                "entry 63 must be readable: record 63 of the 64-entry argument block, or lane 63 "
+                "of the list kernel's culled list (that kernel runs only for n > kInlineSpheres, "
+                "so lane 63's default sphere 63 exists; launch_trace checks n >= 64)");
   auto first_entry = [](uint64_t x) -> uint32_t {
     uint32_t e;
     __asm__("s_ff1_i32_b64 %0, %1" : "=s"(e) : "s"(x));
@@ -544,19 +531,11 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       tacc[r] = tacc[r] + L[r];
     }
   };
-#if SFRT_EXP & 32  // diagnostic build: per-tile visit counters (wrong bytes)
-  uint32_t dbg_visits = 0, dbg_passes = 0, dbg_mode = 0;
-#endif
   auto visit = [&](float cx, float cy, float cz, float rad, float s_pass, int k, float (&L)[R]) {
     float ss[R];
 #pragma unroll
     for (int r = 0; r < R; r++) ss[r] = dist2(px[r], py[r], pz[r], cx, cy, cz);
-#if SFRT_EXP & 32
-    dbg_visits++;
-    dbg_passes += pass_body_r<R>(ss, s_pass, rad, k, L, draw) ? 1u : 0u;
-#else
-    pass_body_r<R>(ss, s_pass, rad, k, L, draw);
-#endif
+    probe.visit(pass_body_r<R>(ss, s_pass, rad, k, L, draw));
   };
   // Every sphere in index order (no culling: cull off, or past kCullSafeIterations steps).
   auto visit_all = [&](float (&L)[R]) {
@@ -601,9 +580,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
       advance(L);
     }
   } else {
-#if SFRT_EXP & 32
-    dbg_mode = 1;
-#endif
+    probe.window_mode();
     float tlo = 0.0f;
     for (; any_marching() && trips < cull_end; ++trips) {
       float L[R];
@@ -674,98 +651,81 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
   // recomputed the 64-bit row offset, three quarter-rate multiplies per slot)
   uint32_t* const row_out = f.out + (long long)(b_s - f.sub_row0) * f.out_pitch;
   auto px_out = [&](int r) { return row_out + col(r); };
-#if SFRT_EXP & 64  // timing probe only (wrong bytes): the march without the shading tail
+  if constexpr (!P::kShade) {  // timing probe (sfrt_probe.h): the march without the shading tail
 #pragma unroll
-  for (int r = 0; r < R; r++)
-    if (valid(r))
-      *px_out(r) =
-          __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^ __float_as_uint(pz[r]) ^ (uint32_t)draw[r];
-#else
-  // Shading: the R records gathered first, then the R texel indices, the R texel
-  // loads back to back, and the stores.  Edge lanes shade their duplicates too
-  // (same values as the real pixel) and store nothing.
-  SphereRec d[R];
+    for (int r = 0; r < R; r++)
+      if (valid(r))
+        probe.march_only(px_out(r), __float_as_uint(px[r]) ^ __float_as_uint(py[r]) ^
+                                        __float_as_uint(pz[r]) ^ (uint32_t)draw[r]);
+  } else {
+    // Shading: the R records gathered first, then the R texel indices, the R texel
+    // loads back to back, and the stores.  Edge lanes shade their duplicates too
+    // (same values as the real pixel) and store nothing.
+    SphereRec d[R];
 #pragma unroll
-  for (int r = 0; r < R; r++)  // draw < n <= 1024: a 32-bit byte offset from the records' base
-    d[r] = *(const SphereRec*)((const char*)sph + (uint32_t)draw[r] * (uint32_t)sizeof(SphereRec));
-  Shading sh[R];
-  PixelDump dl[DUMP ? R : 1];
+    for (int r = 0; r < R; r++)  // draw < n <= 1024: a 32-bit byte offset from the records' base
+      d[r] = *(const SphereRec*)((const char*)sph + (uint32_t)draw[r] * (uint32_t)sizeof(SphereRec));
+    Shading sh[R];
+    PixelDump dl[DUMP ? R : 1];
 #pragma unroll
-  for (int r = 0; r < R; r++)
-    sh[r] = shade_texel(f, d[r], px[r], py[r], pz[r], DUMP ? &dl[DUMP ? r : 0] : nullptr);
-  uint32_t texel[R];
+    for (int r = 0; r < R; r++)
+      sh[r] = shade_texel<P>(f, d[r], px[r], py[r], pz[r], DUMP ? &dl[DUMP ? r : 0] : nullptr);
+    uint32_t texel[R];
 #pragma unroll
-  for (int r = 0; r < R; r++) texel[r] = f.tex[sh[r].tex];
+    for (int r = 0; r < R; r++) texel[r] = f.tex[sh[r].tex];
 #pragma unroll
-  for (int r = 0; r < R; r++) {
-    if (valid(r)) {
-      if (sh[r].outside) atomicOr(f.status, 2);  // the reference would read outside the image
-      const uint32_t rgba = shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
-      *px_out(r) = rgba;
-      if constexpr (DUMP) {
-        const int q = dmp.index[(long long)(b_s - f.sub_row0) * f.sub_w + col(r)];
-        if (q >= 0) {
-          PixelDump& o = dl[r];
-          o.pos[0] = px[r]; o.pos[1] = py[r]; o.pos[2] = pz[r];
-          o.draw = draw[r];
-          o.iters = iters[r];
-          o.rgba = rgba;
-          dmp.out[q] = o;
+    for (int r = 0; r < R; r++) {
+      if (valid(r)) {
+        if (sh[r].outside) atomicOr(f.status, 2);  // the reference would read outside the image
+        const uint32_t rgba = shade_rgba(sh[r].outside ? 0u : texel[r], sh[r].brightness);
+        if constexpr (!DUMP) {
+          *px_out(r) = rgba;
+        } else {  // the listed pixel's record, if it is listed (no frame store)
+          const long long pid = (long long)(b_s - f.sub_row0) * f.sub_w + col(r);
+          int q = 0, qe = dmp.npix;  // first entry >= pid
+          while (q < qe) {
+            const int mid = (q + qe) >> 1;
+            if (dmp.pix[mid] < pid) q = mid + 1;
+            else qe = mid;
+          }
+          if (q < dmp.npix && dmp.pix[q] == pid) {
+            PixelDump& o = dl[r];
+            o.pos[0] = px[r]; o.pos[1] = py[r]; o.pos[2] = pz[r];
+            o.draw = draw[r];
+            o.iters = iters[r];
+            o.rgba = rgba;
+            dmp.out[q] = o;
+          }
         }
       }
     }
   }
-#endif
-#if SFRT_EXP & 32
-  if (lane_s < 5 && valid(0)) {
-    const uint32_t v = lane_s == 0 ? (uint32_t)trips : lane_s == 1 ? dbg_visits : lane_s == 2 ? dbg_passes
-                     : lane_s == 3 ? dbg_mode : (uint32_t)__builtin_popcountll(m);
-    *px_out(0) = v;
-  }
-#endif
-#if SFRT_EXP & 16
-  const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
-#if SFRT_EXP & 1024
-  const uint32_t dbg_trips = (uint32_t)(__builtin_amdgcn_s_memtime() - dbg_c0);
-#else
-  const uint32_t dbg_trips = (uint32_t)trips;
-#endif
-  if (lane < 4 && valid(0)) {
-    const uint32_t v = lane == 0 ? (uint32_t)dbg_t0 : lane == 1 ? (uint32_t)dbg_t1
-                     : lane == 2 ? dbg_trips
-#if SFRT_EXP & 512
-                     : (uint32_t)dbg_entry;
-#else
-                     : (uint32_t)slot;
-#endif
-    *px_out(0) = v;
-  }
-#endif
+  probe.tile_end(px_out(0), lane_s, valid(0), trips, slot, m);
 }
 
 // n <= 64: the records travel in the kernel-argument segment.  8 waves/SIMD: <= 64
 // VGPRs (R = 4 needs 60; measured equal to 7 waves when it spilled one, ab/r2_ab10).
 template <int R>
 __global__ __launch_bounds__(64, 8) void k_trace_window_r(InlineArgs args) {
-  trace_tile_window_r<R, false, false>(args.f, args.s, DumpArgs{});
+  trace_tile_window_r<R, false, false, ActiveProbe>(args.f, args.s, DumpArgs{});
 }
 
 // n > 64: the records in device memory (f.spheres, read with scalar loads: rec_at), the
 // culled list per wave.  57 VGPRs at R = 4 (8 waves/SIMD).
 template <int R>
 __global__ __launch_bounds__(64) void k_trace_window_list(FrameRec f) {
-  trace_tile_window_r<R, true, false>(f, f.spheres, DumpArgs{});
+  trace_tile_window_r<R, true, false, ActiveProbe>(f, f.spheres, DumpArgs{});
 }
 
 // The DUMP instantiations of both (sfrt_world_trace_points): the shipped march and
-// shading, with the float intermediates of listed pixels written out.
+// shading, with the float intermediates of listed pixels written out (never probed).
 template <int R>
 __global__ __launch_bounds__(64) void k_trace_window_r_dump(InlineArgs args, DumpArgs d) {
-  trace_tile_window_r<R, false, true>(args.f, args.s, d);
+  trace_tile_window_r<R, false, true, NoProbe>(args.f, args.s, d);
 }
 template <int R>
 __global__ __launch_bounds__(64) void k_trace_window_list_dump(FrameRec f, DumpArgs d) {
-  trace_tile_window_r<R, true, true>(f, f.spheres, d);
+  trace_tile_window_r<R, true, true, NoProbe>(f, f.spheres, d);
 }
 
 
@@ -797,7 +757,7 @@ static int trace_rays(const FrameRec& f, bool ordered) {
 }
 
 const char* trace_build_flavour() {
-  return SFRT_EXP != 0 ? "diagnostic" : kSlots != 2 ? "ab" : SFRT_BUILD_FLAVOUR;
+  return kDiagnosticBuild ? "diagnostic" : kSlots != 2 ? "ab" : SFRT_BUILD_FLAVOUR;
 }
 
 long long trace_tile_key(const FrameRec& f, long long* tiles) {
@@ -848,6 +808,8 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream,
         default: hipLaunchKernelGGL(k_trace_window_r<4>, gr, b, 0, s, args); break;
       }
     }
+  } else if (f.n < 64) {
+    return -1;  // the list kernel's lookahead reads culled-list lane 63 (a sphere index < n)
   } else if (dump) {
     switch (rays) {
       case 1: hipLaunchKernelGGL(k_trace_window_list_dump<1>, gr, b, 0, s, g, *dump); break;

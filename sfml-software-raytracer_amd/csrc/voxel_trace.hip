@@ -38,23 +38,43 @@ struct V3 {
   float x, y, z;
 };
 
+#ifndef SFRT_VOX_VARIANT
+#define SFRT_VOX_VARIANT 0
+#endif
+
 // blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff
 // the key is non-negative and decodes to an occupied cell of the dense grid.
-// (Staging a one-bit occupancy map of the grid in LDS measured 7-9% slower:
-// these loads hit the caches)
-__device__ __forceinline__ int16_t block_at(const VoxFrame& f, int32_t x, int32_t y, int32_t z) {
+// cell_of gives the cell's index, or -1 for a key outside the grid.
+__device__ __forceinline__ int32_t cell_of(const VoxFrame& f, int32_t x, int32_t y, int32_t z) {
   const int32_t key = (int32_t)(((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z);
-  if (key < 0) return kVoxEmpty;
+  if (key < 0) return -1;
   const int32_t cx = key >> 20, cy = (key >> 10) & 1023, cz = key & 1023;
-  if (cx >= f.nx || cy >= f.ny || cz >= f.nz) return kVoxEmpty;
-  // nx <= 2048, ny, nz <= 1024 (sfrt_voxel_set_blocks): the cell index is below 2^31 and every
-  // factor below 2^24, so 24-bit multiplies and a 32-bit byte offset are exact (the 64-bit
-  // index cost quarter-rate 64-bit multiplies at every DDA step)
+  if (cx >= f.nx || cy >= f.ny || cz >= f.nz) return -1;
+  // nx <= kVoxMaxX, ny <= kVoxMaxY, nz <= kVoxMaxZ (voxel_trace.h, static_asserts there): the
+  // cell index is below 2^31 and every factor below 2^24, so 24-bit multiplies and a 32-bit byte
+  // offset are exact (the 64-bit index cost quarter-rate 64-bit multiplies at every DDA step)
   uint32_t c;  // (cx * ny + cy) * nz + cz by two full-rate v_mad_u32_u24 (left alone, the
                // compiler turns the first into a quarter-rate v_mad_u64_u32)
   __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"((uint32_t)cx), "s"((uint32_t)f.ny), "v"((uint32_t)cy));
   __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(c), "s"((uint32_t)f.nz), "v"((uint32_t)cz));
-  return *(const int16_t*)((const char*)f.blocks + c * 2u);
+  return (int32_t)c;
+}
+
+// Occupancy of a cell (c >= 0): one bit per cell (f.occ, built with the grid), so the DDA's
+// per-step lookup reads a word of a bitmap 16x smaller than the int16 grid -- 12.5 KB for the
+// default 100x10x100 world, resident in the CU's 32 KB L1 where the 200 KB grid is not; the
+// texture id is read only for the cell a ray hits.
+__device__ __forceinline__ bool occupied(const VoxFrame& f, int32_t c) {
+#if SFRT_VOX_VARIANT & 2
+  const uint32_t w = *(const uint32_t*)((const char*)f.occ + (((uint32_t)c >> 3) & ~3u));
+  return (w >> ((uint32_t)c & 31u)) & 1u;
+#else
+  return *(const int16_t*)((const char*)f.blocks + (uint32_t)c * 2u) != kVoxEmpty;
+#endif
+}
+
+__device__ __forceinline__ int16_t block_id(const VoxFrame& f, int32_t c) {
+  return *(const int16_t*)((const char*)f.blocks + (uint32_t)c * 2u);
 }
 
 __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, uint32_t x,
@@ -112,7 +132,8 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
     work++;
-    if (block_at(f, pix, piy, piz) != kVoxEmpty) return false;
+    const int32_t cell = cell_of(f, pix, piy, piz);
+    if (cell >= 0 && occupied(f, cell)) return false;
     const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
     const float c = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
@@ -153,6 +174,9 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   const float yx = RECIP ? 1.0f / lx : 0.0f, yy = RECIP ? 1.0f / ly : 0.0f,
               yz = RECIP ? 1.0f / lz : 0.0f;
   int DI = 0;
+#if SFRT_VOX_VARIANT & 1
+  float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // NaN: never >=
+#endif
   float raySpeed = 0.0f;
   int colRay = 0;
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
@@ -182,7 +206,13 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     const float tryDist = dist + raySpeed;
 
     // dynamic billboards in front of the next block (World.cpp:353-378)
+#if SFRT_VOX_VARIANT & 1
+    // the next billboard's distance is held in a register (NaN past the last): the
+    // while test reads no memory on the steps that pass no billboard (nearly all)
+    while (tryDist >= dnext) {
+#else
     while (DI < f.ndyn && tryDist >= f.dyn[DI].dist) {
+#endif
       const VoxDyn& d = f.dyn[DI];
       raySpeed = d.dist - dist;
       dist = d.dist;
@@ -211,13 +241,17 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
         }
       }
       DI++;
+#if SFRT_VOX_VARIANT & 1
+      dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf("");
+#endif
     }
 
     dist = tryDist;
     pos = tryPos;
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
-    const int16_t id = block_at(f, pix, piy, piz);
-    if (id != kVoxEmpty) {  // hit a block (World.cpp:385)
+    const int32_t cell = cell_of(f, pix, piy, piz);
+    if (cell >= 0 && occupied(f, cell)) {  // hit a block (World.cpp:385)
+      const int16_t id = block_id(f, cell);
       uint32_t c;
       if (id < 0) {
         c = f.colors[-id];

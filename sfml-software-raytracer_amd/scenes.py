@@ -166,7 +166,23 @@ CONFIGS = {
     "c4_7680x4320_default10": (7680, 4320, "default10", [(0.0, 0.0)]),
     "c4_7680x4320_lcg64": (7680, 4320, "lcg64", [(0.0, 0.0)]),
     "c5_16384x16384_default10": (16384, 16384, "default10", [(0.0, 0.0)]),
+    "c5_16384x16384_lcg64": (16384, 16384, "lcg64", [(0.0, 0.0)]),
+    # bench.py --gpus N's weak-scaling frame (3840 x 2160*N, 64 spheres) at N = 2, 4, 8: the
+    # gathered headline frames of the driver's SCALE run, pinned like the configs above
+    "w2_3840x4320_lcg64": (3840, 4320, "lcg64", [(0.0, 0.0)]),
+    "w4_3840x8640_lcg64": (3840, 8640, "lcg64", [(0.0, 0.0)]),
+    "w8_3840x17280_lcg64": (3840, 17280, "lcg64", [(0.0, 0.0)]),
+    # beyond the reference's scene sizes: the n > 64 kernel's bench line (bench.py also)
+    "x_3840x2160_lcg256": (3840, 2160, "lcg256", [(0.0, 0.0)]),
 }
+
+
+def golden_key(width: int, height: int, scene: str, pose=(0.0, 0.0)):
+    """The tests/golden/golden.json "frames" key of a (frame size, scene, pose), or None."""
+    for cfg, (w, h, s, poses) in CONFIGS.items():
+        if (w, h, s) == (width, height, scene) and tuple(pose) in poses:
+            return f"{cfg}@{pose[0]:g},{pose[1]:g}"
+    return None
 
 # FNV-1a-64 frame hashes the survey recorded from the unmodified reference TU
 # (SURVEY.md section 6, BASELINE.md).  Key: (config, pose).

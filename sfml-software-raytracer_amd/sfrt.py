@@ -55,7 +55,8 @@ ABI_SYMBOLS = (
     "sfrt_multi_bands", "sfrt_multi_render", "sfrt_multi_check", "sfrt_multi_update_image",
     "sfrt_world_row_costs", "sfrt_multi_cost_bands", "sfrt_multi_row_costs", "sfrt_multi_balance",
     "sfrt_multi_set_transfer", "sfrt_multi_get_transfer", "sfrt_band_packed_bytes", "sfrt_band_pack",
-    "sfrt_band_unpack", "sfrt_world_alpha_binary",
+    "sfrt_band_unpack", "sfrt_world_alpha_binary", "sfrt_multi_transport_library",
+    "sfrt_multi_use_test_transport",
 )
 
 SFRT_MULTI_AUTO, SFRT_MULTI_RCCL, SFRT_MULTI_PEER = 0, 1, 2
@@ -191,6 +192,8 @@ def lib() -> ctypes.CDLL:
         "sfrt_band_unpack": ([vp, ctypes.c_int64, vp, vp], c_int),
         "sfrt_world_alpha_binary": ([W, P(c_int)], c_int),
         "sfrt_multi_update_image": ([vp, vp], c_int),
+        "sfrt_multi_transport_library": ([ctypes.c_char_p, c_int], c_int),
+        "sfrt_multi_use_test_transport": ([ctypes.c_char_p], c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -522,6 +525,20 @@ def band_unpack(src_ptr: int, pixels: int, dst_ptr: int, stream: int = 0) -> Non
     """sfrt_band_unpack: the packed transfer format -> RGBA8 device pixels (asynchronous)."""
     _check(lib().sfrt_band_unpack(ctypes.c_void_p(src_ptr), int(pixels), ctypes.c_void_p(dst_ptr),
                                   ctypes.c_void_p(stream or None)), "band_unpack")
+
+
+def multi_transport_library() -> str:
+    """sfrt_multi_transport_library: "" before the first RCCL context, else the library behind
+    SFRT_MULTI_RCCL ("librccl.so.1", or "test:<path>" for a test transport)."""
+    buf = ctypes.create_string_buffer(4096)
+    _check(lib().sfrt_multi_transport_library(buf, len(buf)), "sfrt_multi_transport_library")
+    return buf.value.decode()
+
+
+def use_test_transport(path: str) -> None:
+    """TEST ONLY (sfrt_multi_use_test_transport): the RCCL C API from `path`, before the
+    process's first RCCL context."""
+    _check(lib().sfrt_multi_use_test_transport(path.encode()), "sfrt_multi_use_test_transport")
 
 
 def multi_bands(height: int, n: int, root_factor: float = 1.0) -> list[tuple[int, int]]:

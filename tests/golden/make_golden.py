@@ -49,7 +49,8 @@ def glsl_section(threads):
     sec = {}
     for key, w, h, make in GLSL_CASES:
         frame = oracle.GlslOracle(make(w, h), *floor).render(w, h, threads)
-        sec[key] = {"width": w, "height": h, "fnv1a64": oracle.fnv1a64(frame)}
+        sec[key] = {"width": w, "height": h, "fnv1a64": oracle.fnv1a64(frame),
+                    "sha256": hashlib.sha256(frame.tobytes()).hexdigest()}
         print("glsl", key, sec[key]["fnv1a64"], flush=True)
     return sec
 
@@ -61,7 +62,8 @@ def all_textures_section(threads):
     sec = {}
     for case in CASES:
         frame = tex_oracle(*case).render(threads)
-        sec[key(*case)] = {"fnv1a64": oracle.fnv1a64(frame)}
+        sec[key(*case)] = {"fnv1a64": oracle.fnv1a64(frame),
+                           "sha256": hashlib.sha256(frame.tobytes()).hexdigest()}
         print("all_textures", key(*case), sec[key(*case)]["fnv1a64"], flush=True)
     return sec
 
@@ -121,7 +123,8 @@ def main():
         frame = o.render(threads)
         out["voxel"][case_key(case)] = {"width": w, "height": h, "cam_pos": list(p),
                                         "rotation": r, "hrotation": hr,
-                                        "fnv1a64": oracle.fnv1a64(frame)}
+                                        "fnv1a64": oracle.fnv1a64(frame),
+                                        "sha256": hashlib.sha256(frame.tobytes()).hexdigest()}
         print("voxel", case_key(case), out["voxel"][case_key(case)]["fnv1a64"], flush=True)
     for name, fn in SECTIONS.items():
         out[name] = fn(threads)

@@ -3,7 +3,8 @@
 // branch (ncclCommInitAll, in-place ncclGather, grouped ncclSend/ncclRecv, packed
 // send -> unpack) runs with n > 1 ranks on a one-GPU box.  Real RCCL refuses a device
 // listed twice in ncclCommInitAll; this library accepts it.  Loaded by libsfrt.so in
-// place of librccl.so.1 when SFRT_RCCL_LIB names it (tests/test_gpu_bands.py).
+// place of librccl.so.1 after an explicit sfrt_multi_use_test_transport(path) call made
+// before the process's first RCCL context (tests/test_gpu_bands.py).
 //
 // Ordering contract (RCCL's, for what sfrt_multi relies on): an operation queued on a
 // rank's stream starts after the work queued on that stream before it, and every

@@ -18,7 +18,8 @@ import scenes
 from conftest import ROOT, host_threads
 
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
-CASES = [(1920, 1080, (0.0, 0.0)), (3840, 2160, (1.1, -0.2))]
+# the 4K pose (0, 0) case is bench.py's "3840x2160_lcg64_all_textures" line
+CASES = [(1920, 1080, (0.0, 0.0)), (3840, 2160, (1.1, -0.2)), (3840, 2160, (0.0, 0.0))]
 
 
 def key(w, h, pose):

@@ -26,7 +26,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world_size, port, width, height, out_path, factor=1.0):
+def _worker(rank, world_size, port, width, height, out_path, factor=1.0, staged=False):
     import sys
     for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), os.path.join(ROOT, "oracle"), ROOT):
         sys.path.insert(0, p)
@@ -35,6 +35,8 @@ def _worker(rank, world_size, port, width, height, out_path, factor=1.0):
     import scenes
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world_size)
+    if staged:  # bench.py --rehearse: point-to-point transfers through host copies
+        bands.stage_p2p_through_host()
     tex, tw, th = scenes.load_floor()
     pitch = width * 4
     poses = [(0.4, 0.05), (1.3, -0.2), (2.9, 0.3)]
@@ -55,11 +57,14 @@ def _worker(rank, world_size, port, width, height, out_path, factor=1.0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world_size,height,factor", [(2, 90, 1.0), (3, 100, 1.0), (2, 90, 2.5),
-                                                      (3, 100, 1.5)])
-def test_row_band_gather_matches_single_rank(tmp_path, world_size, height, factor):
+@pytest.mark.parametrize("world_size,height,factor,staged", [
+    (2, 90, 1.0, False), (3, 100, 1.0, False), (2, 90, 2.5, False), (3, 100, 1.5, False),
+    (3, 100, 1.5, True), (4, 120, 2.0, True)])
+def test_row_band_gather_matches_single_rank(tmp_path, world_size, height, factor, staged):
+    """staged: the host-staged point-to-point stand-in of bench.py --rehearse
+    (bands.stage_p2p_through_host), unequal bands so that every band crosses it."""
     out = str(tmp_path / "ok.npy")
-    mp.start_processes(_worker, args=(world_size, _free_port(), 160, height, out, factor),
+    mp.start_processes(_worker, args=(world_size, _free_port(), 160, height, out, factor, staged),
                        nprocs=world_size, start_method="spawn", join=True)
     assert bool(np.load(out)[0])
 

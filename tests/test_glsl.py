@@ -36,6 +36,8 @@ GLSL_CASES = [
     ("random2(12,2,14)@320x180", 320, 180, lambda w, h: gs.random_uniforms(2, 12, 2, 14, w, h)),
     ("random3(40,4,50)@640x360", 640, 360, lambda w, h: gs.random_uniforms(3, 40, 4, 50, w, h)),
     ("random4(5,0,9)@333x97", 333, 97, lambda w, h: gs.random_uniforms(4, 5, 0, 9, w, h)),
+    # bench.py's "glsl_3840x2160" line (its 1080p line is default@1920x1080)
+    ("default@3840x2160", 3840, 2160, lambda w, h: gs.default_uniforms(w, h)),
 ]
 CPU_CASES = [c for c in GLSL_CASES if c[1] * c[2] <= 640 * 360]
 

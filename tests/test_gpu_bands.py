@@ -95,7 +95,7 @@ def _band_worker(rank, world_size, port, key, factor, frames, out_path):
     ("c4_7680x4320_default10@0,0", 2, 1.0), ("c4_7680x4320_default10@0,0", 4, 1.0),
     ("c4_7680x4320_lcg64@0,0", 2, 2.5), ("c4_7680x4320_default10@0,0", 4, 2.0),
     ("c4_7680x4320_lcg64@0,0", 4, "cost:1.0"), ("c4_7680x4320_default10@0,0", 2, "cost:2.0"),
-    ("c5_16384x16384_default10@0,0", 8, 1.0)])
+    ("c5_16384x16384_default10@0,0", 8, 1.0), ("c5_16384x16384_lcg64@0,0", 8, 1.0)])
 def test_distributed_bands_match_golden(tmp_path, key, world_size, factor):
     """world_size ranks on cuda:0, HIP-rendered bands, gathered to rank 0 by BandPipeline
     (two frames in flight for config 4): the frames hash to the single-frame golden value."""
@@ -121,7 +121,7 @@ def _multi(devices, transport, floor_tex):
 @pytest.mark.parametrize("key,n,factor", [
     ("c4_7680x4320_lcg64@0,0", 2, 1.0), ("c4_7680x4320_lcg64@0,0", 4, 1.0),
     ("c4_7680x4320_default10@0,0", 2, 2.5), ("c4_7680x4320_default10@0,0", 4, 2.0),
-    ("c5_16384x16384_default10@0,0", 8, 1.0)])
+    ("c5_16384x16384_default10@0,0", 8, 1.0), ("c5_16384x16384_lcg64@0,0", 8, 2.0)])
 def test_multi_peer_matches_golden(floor_tex, key, n, factor):
     """sfrt_multi over devices [0] * n (peer copies into devices[0]'s frame): the host frame
     of sfrt_multi_update_image hashes to the golden value, equal and root-weighted bands."""
@@ -156,9 +156,9 @@ def test_multi_rccl_one_gpu_matches_oracle(floor_tex):
         sfrt.Multi([0, 0], sfrt.SFRT_MULTI_RCCL)
 
 
-def _rccl_loopback_worker(_rank, cases, out_path):
-    """A fresh process whose environment names the loopback transport (SFRT_RCCL_LIB):
-    sfrt_multi's RCCL branch over devices [0] * n, n > 1."""
+def _rccl_loopback_worker(_rank, lib_path, cases, out_path):
+    """A fresh process that selects the loopback transport before its first RCCL context
+    (sfrt_multi_use_test_transport): sfrt_multi's RCCL branch over devices [0] * n, n > 1."""
     import ctypes
     import sys
     for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), os.path.join(ROOT, "oracle"), ROOT):
@@ -169,7 +169,9 @@ def _rccl_loopback_worker(_rank, cases, out_path):
     import sfrt
     torch.cuda.set_device(0)
     floor = sc.load_floor()
-    stats = ctypes.CDLL(os.environ["SFRT_RCCL_LIB"]).rccl_loopback_stats
+    assert sfrt.multi_transport_library() == ""
+    sfrt.use_test_transport(lib_path)
+    stats = ctypes.CDLL(lib_path).rccl_loopback_stats
     st = (ctypes.c_longlong * 5)()
     res = []
     for key, n, mode in cases:
@@ -219,33 +221,41 @@ def _rccl_loopback_worker(_rank, cases, out_path):
         res.append({"case": [key, n, mode], "ok": all(h == g["fnv1a64"] for h in hashes),
                     "stats": list(st), "packed": m.transfer()[1]})
         m.close()
+    res.append({"library": sfrt.multi_transport_library(), "late_switch_refused": False})
+    try:
+        sfrt.use_test_transport(lib_path)
+    except sfrt.SfrtError:
+        res[-1]["late_switch_refused"] = True
     with open(out_path, "w") as fh:
         json.dump(res, fh)
 
 
-def test_multi_rccl_branch_n_ranks_loopback(floor_tex, tmp_path, monkeypatch):
+def test_multi_rccl_branch_n_ranks_loopback(floor_tex, tmp_path):
     """sfrt_multi's RCCL branch with n = 2, 4 (config 4) and 8 (config 5) ranks: RCCL refuses a
     device listed twice, so on a one-GPU box the branch runs over the tests' loopback transport
     (tests/native/rccl_loopback.cpp: the RCCL C API -- ncclCommInitAll, group start/end,
-    ncclGather, ncclSend/ncclRecv -- as HIP peer copies with RCCL's stream ordering) loaded
-    through SFRT_RCCL_LIB.  Equal bands with RGBA8 transfers take the in-place ncclGather;
+    ncclGather, ncclSend/ncclRecv -- as HIP peer copies with RCCL's stream ordering) selected by
+    sfrt_multi_use_test_transport (reported by sfrt_multi_transport_library, refused once
+    the process resolved its transport).  Equal bands with RGBA8 transfers take the in-place ncclGather;
     root-weighted and cost-weighted bands the grouped send/recv; packed transfers send the
     packed bands and unpack on the root.  Every frame hashes to the golden value; six
     pipelined frames with the camera turning equal one-GPU frames."""
     import __graft_entry__ as g
     lib = g.build_loopback()
-    monkeypatch.setenv("SFRT_RCCL_LIB", lib)
     cases = [("c4_7680x4320_lcg64@0,0", 2, "equal/rgba"), ("c4_7680x4320_lcg64@0,0", 4, "equal/rgba"),
              ("c4_7680x4320_default10@0,0", 2, "equal/packed"),
              ("c4_7680x4320_lcg64@0,0", 4, "root:2.5/rgba"), ("c4_7680x4320_default10@0,0", 4, "root:2.0/packed"),
              ("c4_7680x4320_lcg64@0,0", 4, "cost:1.5/packed"), ("c4_7680x4320_default10@0,0", 2, "cost:1.0/rgba"),
              ("c5_16384x16384_default10@0,0", 8, "equal/rgba"), ("c5_16384x16384_default10@0,0", 8, "root:2.0/packed"),
+             ("c5_16384x16384_lcg64@0,0", 8, "equal/rgba"),
              ("pipelined", 3, "packed"), ("pipelined", 4, "rgba")]
     out = str(tmp_path / "res.json")
-    mp.start_processes(_rccl_loopback_worker, args=(cases, out), nprocs=1, start_method="spawn",
+    mp.start_processes(_rccl_loopback_worker, args=(lib, cases, out), nprocs=1, start_method="spawn",
                        join=True)
     res = json.load(open(out))
-    assert len(res) == len(cases)
+    assert len(res) == len(cases) + 1
+    assert res[-1] == {"library": "test:" + lib, "late_switch_refused": True}, res[-1]
+    res = res[:-1]
     prev = [0] * 5
     for r, (key, n, mode) in zip(res, cases):
         assert r["ok"], r

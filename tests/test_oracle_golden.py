@@ -53,7 +53,11 @@ def test_iteration_statistics_match_reference_probe(floor, cfg, pose):
         assert int(it.max()) == want["max"]
 
 
-FRAME_KEYS = sorted(GOLDEN["frames"])
+# The CPU suite re-renders golden frames up to 8K (a few seconds each on 8 cores); the larger
+# ones (16384^2, the 3840 x 8640 / 17280 weak-scaling frames) take minutes on the oracle and
+# are checked where they are used: the GPU frame against the hash (test_gpu_parity.py
+# test_large_frame_matches_golden_hash, test_gpu_bands.py, bench.py's bit_identical fields).
+FRAME_KEYS = sorted(k for k, g in GOLDEN["frames"].items() if g["width"] * g["height"] <= 7680 * 4320)
 
 
 @pytest.mark.parametrize("key", FRAME_KEYS)

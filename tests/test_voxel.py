@@ -24,6 +24,7 @@ VOXEL_CASES = [  # (width, height, cam_pos, rotation, hrotation)
     (1920, 1080, (15.5, 1.9, 15.5), 0.0, 0.0),
     (1920, 1080, (30.25, 2.6, 12.75), 2.2, 0.25),
     (3840, 2160, (47.5, 1.5, 60.1), 4.0, -0.3),
+    (3840, 2160, (15.5, 1.9, 15.5), 0.0, 0.0),  # bench.py's "voxel_3840x2160" line
 ]
 
 

@@ -25,7 +25,39 @@ CASES = {
     "8k": (7680, 4320, "lcg64", (0.0, 0.0), False),
     "1080": (1920, 1080, "default10", (0.0, 0.0), False),
     "4k_256": (3840, 2160, "lcg256", (0.0, 0.0), False),
+    # the other renderers: scene = "voxel:<x>,<y>,<z>" / "glsl", pose = rot
+    "vox1080": (1920, 1080, "voxel:15.5,1.9,15.5", (0.0, 0.0), False),
+    "vox4k": (3840, 2160, "voxel:15.5,1.9,15.5", (0.0, 0.0), False),
+    "vox4k_rot": (3840, 2160, "voxel:47.5,1.5,60.1", (4.0, -0.3), False),
+    "glsl1080": (1920, 1080, "glsl", (0.0, 0.0), False),
+    "glsl4k": (3840, 2160, "glsl", (0.0, 0.0), False),
 }
+
+
+def renderer(sfrt, scenes, sname, pose, width, height, rays):
+    """An object with render_band(ptr, pitch, row0, rows, stream) / check(stream) for a case."""
+    if sname.startswith("voxel:"):
+        import voxel_scenes as vs
+        v = sfrt.VoxelWorld(0)
+        tex, dyn = vs.load_textures()
+        v.load_assets(tex, dyn, vs.COLORS)
+        v.set_scene(vs.default_world(tuple(float(c) for c in sname[6:].split(",")), *pose),
+                    width, height)
+        return v, None
+    if sname == "glsl":
+        import glsl_scenes as gs
+        g = sfrt.GlslShader(0)
+        g.set_ground(*scenes.load_floor())
+        g.set_uniforms(gs.default_uniforms(width, height, *pose))
+
+        class Draw:
+            def render_band(self, ptr, pitch, row0, rows, stream):
+                g.draw(ptr, width, height, pitch, row0, rows, stream)
+
+            def check(self, stream):
+                g.check(stream)
+        return Draw(), g
+    return None, None
 
 
 def child(cases, reps, rays):
@@ -49,10 +81,14 @@ def child(cases, reps, rays):
     torch.cuda.synchronize()
     gap = float(np.median([a.elapsed_time(b) for a, b in pairs]))
     out = {}
+    sphere_world = w
     for name in cases:
         width, height, sname, pose, turn = CASES[name]
-        sc = scenes.SCENES[sname]().posed(*pose)
-        w.set_scene(sc, width, height)
+        w, keep = renderer(sfrt, scenes, sname, pose, width, height, rays)
+        if w is None:
+            w = sphere_world
+            sc = scenes.SCENES[sname]().posed(*pose)
+            w.set_scene(sc, width, height)
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
         for k in range(20):  # warm-up (clock ramp, tile-order chain)
             if turn:

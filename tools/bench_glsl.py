@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--orders", default="0",
                     help="SFRT_OPT_TILE_ORDER values (0 row-major = the default here, 1 adaptive; "
                          "keys get /ordered)")
+    ap.add_argument("--set", choices=("all", "bench"), default="all",
+                    help="bench: only the two frames bench.py times (1080p and 4K, rot (0,0)), "
+                         "one frame per launch size (rocprof summaries per launch size)")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -37,8 +40,8 @@ def main():
     s.set_ground(*floor)
     res = {}
     threads = max(1, min(16, os.cpu_count() or 1))
-    for width, height, rot, frames in [(1920, 1080, (0.0, 0.0), 0), (3840, 2160, (0.0, 0.0), 0),
-                                       (3840, 2160, (5.5, -0.4), 300)]:
+    cases = [(1920, 1080, (0.0, 0.0), 0), (3840, 2160, (0.0, 0.0), 0), (3840, 2160, (5.5, -0.4), 300)]
+    for width, height, rot, frames in (cases[:2] if args.set == "bench" else cases):
         u = gs.default_uniforms(width, height, *rot, frames=frames)
         s.set_uniforms(u)
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")

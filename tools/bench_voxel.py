@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--orders", default="0",
                     help="comma list of SFRT_OPT_TILE_ORDER values (0 row-major = the default "
                          "here, 1 adaptive; entries get /ordered)")
+    ap.add_argument("--set", choices=("all", "bench"), default="all",
+                    help="bench: only the two frames bench.py times (1080p and 4K at the default "
+                         "pose), one frame per launch size, so that rocprof summaries per launch "
+                         "size map 1:1 to bench lines")
     args = ap.parse_args()
     import oracle  # CPU baseline / checker only
     stream = torch.cuda.Stream()
@@ -39,6 +43,8 @@ def main():
     frames = [(1920, 1080, ((15.5, 1.9, 15.5), 0.0, 0.0)),
               (3840, 2160, ((15.5, 1.9, 15.5), 0.0, 0.0)),
               (3840, 2160, ((47.5, 1.5, 60.1), 4.0, -0.3))]
+    if args.set == "bench":
+        frames = frames[:2]
     runs = [(wd, ht, ps, od) for wd, ht, ps in frames
             for od in [int(x) for x in args.orders.split(",")]]
     for width, height, pose, order in runs:

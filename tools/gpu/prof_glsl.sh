@@ -1,14 +1,14 @@
-# Kernel trace + PMC passes of tools/bench_voxel.py (profiles/<tag>_voxel_*):
-#   /usr/local/graft/bin/gpurun --timeout 900 -- "TAG=r2m bash tools/gpu/prof_voxel.sh"
-# then: python tools/rocprof_summary.py --kernel k_voxel --trace gpurun_out/$TAG/trace
+# Kernel trace + PMC passes of tools/bench_glsl.py (profiles/<tag>_glsl_*):
+#   /usr/local/graft/bin/gpurun --timeout 900 -- "TAG=r4a bash tools/gpu/prof_glsl.sh"
+# then: python tools/rocprof_summary.py --kernel k_glsl --trace gpurun_out/$TAG/trace
 #       --fetch gpurun_out/$TAG/pmc_fetch --write gpurun_out/$TAG/pmc_write
-#       --sq gpurun_out/$TAG/pmc_sq gpurun_out/$TAG/pmc_sq2 --tag ${TAG}_voxel
+#       --sq gpurun_out/$TAG/pmc_sq gpurun_out/$TAG/pmc_sq2 --tag ${TAG}_glsl
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-profvox}
+O=gpurun_out/${TAG:-profglsl}
 mkdir -p $O
-B="tools/bench_voxel.py --no-cpu --steps 20 --set bench"
+B="tools/bench_glsl.py --no-cpu --steps 20 --set bench"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python $B > $O/trace.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python $B > $O/pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python $B > $O/pmc_write.log 2>&1 || exit 1
