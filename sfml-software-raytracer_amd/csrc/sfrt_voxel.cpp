@@ -74,8 +74,6 @@ struct sfrt_voxel {
   DevTex tex[sfrt::kVoxSlots], dyn_tex[sfrt::kVoxSlots];
   int16_t* d_blocks = nullptr;
   size_t d_blocks_cap = 0;
-  uint32_t* d_occ = nullptr;  // occupancy bitmap of the grid (VoxFrame::occ)
-  size_t d_occ_cap = 0;
   bool blocks_dirty = true;
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
@@ -107,7 +105,6 @@ struct sfrt_voxel {
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
     (void)hipFree(d_blocks);
-    (void)hipFree(d_occ);
     for (auto& t : slots) {
       (void)hipFree(t.d);
       (void)hipHostFree(t.h);
@@ -209,23 +206,11 @@ struct sfrt_voxel {
       }
       HIP_TRY(hipMemcpy(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
                         hipMemcpyHostToDevice));
-      std::vector<uint32_t> occ((blocks.size() + 31) / 32, 0u);
-      for (size_t k = 0; k < blocks.size(); k++)
-        if (blocks[k] != sfrt::kVoxEmpty) occ[k >> 5] |= 1u << (k & 31);
-      if (d_occ_cap < occ.size()) {
-        (void)hipFree(d_occ);
-        d_occ = nullptr;
-        d_occ_cap = 0;
-        HIP_TRY(hipMalloc(&d_occ, occ.size() * sizeof(uint32_t)));
-        d_occ_cap = occ.size();
-      }
-      HIP_TRY(hipMemcpy(d_occ, occ.data(), occ.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
       blocks_dirty = false;
     }
     f.col = (const float*)d;
     f.row = (const float*)(d + b_col);
     f.blocks = d_blocks;
-    f.occ = d_occ;
     f.nx = nx; f.ny = ny; f.nz = nz;
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
       f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};

@@ -17,7 +17,7 @@ constexpr int kVoxSlots = 10;              // textures / dynTextures / colors (W
 constexpr int16_t kVoxEmpty = -32768;
 // Dense block grid limits (sfrt_voxel_set_blocks refuses larger grids): the reference's map key
 // (x << 20) + (y << 10) + z (World.cpp:385) addresses x < 2048, y, z < 1024 without overlap, and
-// block_at (voxel_trace.hip) indexes the grid with two 24-bit multiplies and a 32-bit byte
+// cell_hit (voxel_trace.hip) indexes the grid with two 24-bit multiplies and a 32-bit byte
 // offset, exact only under these bounds.
 constexpr int kVoxMaxX = 2048, kVoxMaxY = 1024, kVoxMaxZ = 1024;
 static_assert(kVoxMaxX <= (1 << 24) && kVoxMaxY <= (1 << 24) && kVoxMaxZ <= (1 << 24),
@@ -58,7 +58,6 @@ struct VoxFrame {
   const float* col;                         // per column i: dir.x, dir.z, atan2f(dir.z, dir.x)
   const float* row;                         // per row j: dir.y, yscale
   const int16_t* blocks;                    // dense [nx][ny][nz], textureID or kVoxEmpty
-  const uint32_t* occ;                      // one bit per cell of `blocks`: != kVoxEmpty
   int32_t nx, ny, nz;
   VoxTex tex[kVoxSlots];
   VoxTex dyn_tex[kVoxSlots];

@@ -38,43 +38,30 @@ struct V3 {
   float x, y, z;
 };
 
-#ifndef SFRT_VOX_VARIANT
-#define SFRT_VOX_VARIANT 0
-#endif
-
-// blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff
-// the key is non-negative and decodes to an occupied cell of the dense grid.
-// cell_of gives the cell's index, or -1 for a key outside the grid.
-__device__ __forceinline__ int32_t cell_of(const VoxFrame& f, int32_t x, int32_t y, int32_t z) {
-  const int32_t key = (int32_t)(((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z);
-  if (key < 0) return -1;
-  const int32_t cx = key >> 20, cy = (key >> 10) & 1023, cz = key & 1023;
-  if (cx >= f.nx || cy >= f.ny || cz >= f.nz) return -1;
-  // nx <= kVoxMaxX, ny <= kVoxMaxY, nz <= kVoxMaxZ (voxel_trace.h, static_asserts there): the
-  // cell index is below 2^31 and every factor below 2^24, so 24-bit multiplies and a 32-bit byte
-  // offset are exact (the 64-bit index cost quarter-rate 64-bit multiplies at every DDA step)
-  uint32_t c;  // (cx * ny + cy) * nz + cz by two full-rate v_mad_u32_u24 (left alone, the
-               // compiler turns the first into a quarter-rate v_mad_u64_u32)
-  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"((uint32_t)cx), "s"((uint32_t)f.ny), "v"((uint32_t)cy));
-  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(c), "s"((uint32_t)f.nz), "v"((uint32_t)cz));
-  return (int32_t)c;
+// blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff the key is
+// non-negative and decodes to an occupied cell of the dense grid.  Branch-free: a negative key
+// has cx = key >> 20 (logical) >= 2048 >= nx, so three unsigned compares decide validity alone;
+// the index (cx * ny + cy) * nz + cz is computed for every lane and an invalid lane reads cell 0
+// (in bounds) -- no exec-mask branches around the per-step lookup (profiles/ab/r4_ab1).
+// nx <= kVoxMaxX, ny <= kVoxMaxY, nz <= kVoxMaxZ (voxel_trace.h, static_asserts there): for a
+// valid cell every factor is below 2^24 and the index below 2^31, so two full-rate
+// v_mad_u32_u24 and a 32-bit byte offset are exact (left alone, the compiler turns the first
+// into a quarter-rate v_mad_u64_u32).  `cell` is the index for block_id when the cell is hit.
+__device__ __forceinline__ bool cell_hit(const VoxFrame& f, int32_t x, int32_t y, int32_t z,
+                                         uint32_t& cell) {
+  const uint32_t key = ((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z;
+  const uint32_t cx = key >> 20, cy = (key >> 10) & 1023u, cz = key & 1023u;
+  const bool valid = (cx < (uint32_t)f.nx) & (cy < (uint32_t)f.ny) & (cz < (uint32_t)f.nz);
+  uint32_t c;
+  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(cx), "s"((uint32_t)f.ny), "v"(cy));
+  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(c), "s"((uint32_t)f.nz), "v"(cz));
+  c = valid ? c : 0u;
+  cell = c;
+  return valid & (*(const int16_t*)((const char*)f.blocks + c * 2u) != kVoxEmpty);
 }
 
-// Occupancy of a cell (c >= 0): one bit per cell (f.occ, built with the grid), so the DDA's
-// per-step lookup reads a word of a bitmap 16x smaller than the int16 grid -- 12.5 KB for the
-// default 100x10x100 world, resident in the CU's 32 KB L1 where the 200 KB grid is not; the
-// texture id is read only for the cell a ray hits.
-__device__ __forceinline__ bool occupied(const VoxFrame& f, int32_t c) {
-#if SFRT_VOX_VARIANT & 2
-  const uint32_t w = *(const uint32_t*)((const char*)f.occ + (((uint32_t)c >> 3) & ~3u));
-  return (w >> ((uint32_t)c & 31u)) & 1u;
-#else
-  return *(const int16_t*)((const char*)f.blocks + (uint32_t)c * 2u) != kVoxEmpty;
-#endif
-}
-
-__device__ __forceinline__ int16_t block_id(const VoxFrame& f, int32_t c) {
-  return *(const int16_t*)((const char*)f.blocks + (uint32_t)c * 2u);
+__device__ __forceinline__ int16_t block_id(const VoxFrame& f, uint32_t c) {
+  return *(const int16_t*)((const char*)f.blocks + c * 2u);
 }
 
 __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, uint32_t x,
@@ -132,8 +119,8 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
     work++;
-    const int32_t cell = cell_of(f, pix, piy, piz);
-    if (cell >= 0 && occupied(f, cell)) return false;
+    uint32_t cell;
+    if (cell_hit(f, pix, piy, piz, cell)) return false;
     const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
     const float c = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
@@ -174,9 +161,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   const float yx = RECIP ? 1.0f / lx : 0.0f, yy = RECIP ? 1.0f / ly : 0.0f,
               yz = RECIP ? 1.0f / lz : 0.0f;
   int DI = 0;
-#if SFRT_VOX_VARIANT & 1
-  float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // NaN: never >=
-#endif
+  float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // next billboard; NaN: never >=
   float raySpeed = 0.0f;
   int colRay = 0;
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
@@ -184,35 +169,24 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     const float xray = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float yray = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
     const float zray = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
-    if (xray <= yray && xray <= zray) {
-      raySpeed = xray;
-      tryPos.x += dir.x * (raySpeed + 0.002f);
-      tryPos.y += dir.y * raySpeed;
-      tryPos.z += dir.z * raySpeed;
-      colRay = 1;
-    } else if (yray <= xray && yray <= zray) {
-      raySpeed = yray;
-      tryPos.x += dir.x * raySpeed;
-      tryPos.y += dir.y * (raySpeed + 0.002f);
-      tryPos.z += dir.z * raySpeed;
-      colRay = 2;
-    } else {
-      raySpeed = zray;
-      tryPos.x += dir.x * raySpeed;
-      tryPos.y += dir.y * raySpeed;
-      tryPos.z += dir.z * (raySpeed + 0.002f);
-      colRay = 3;
-    }
+    // the reference's if / else-if / else (World.cpp:330-350) as selects: one branch-free step
+    // (as branches the compiler built an exec-mask diamond with ~12 scalar instructions)
+    const bool ax = (xray <= yray) & (xray <= zray);
+    const bool ay = !ax & (yray <= xray) & (yray <= zray);
+    raySpeed = ax ? xray : (ay ? yray : zray);
+    const float rs2 = raySpeed + 0.002f;
+    tryPos.x += dir.x * (ax ? rs2 : raySpeed);
+    tryPos.y += dir.y * (ay ? rs2 : raySpeed);
+    tryPos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
+    colRay = ax ? 1 : (ay ? 2 : 3);
     const float tryDist = dist + raySpeed;
 
     // dynamic billboards in front of the next block (World.cpp:353-378)
-#if SFRT_VOX_VARIANT & 1
-    // the next billboard's distance is held in a register (NaN past the last): the
-    // while test reads no memory on the steps that pass no billboard (nearly all)
-    while (tryDist >= dnext) {
-#else
-    while (DI < f.ndyn && tryDist >= f.dyn[DI].dist) {
-#endif
+    // the next billboard's distance is held in a register (NaN past the last), so the test
+    // reads no memory on the steps that pass no billboard (nearly all; it was a dependent
+    // global load at every step), and a wave whose lanes all pass none skips the loop
+    if (__builtin_amdgcn_ballot_w64(tryDist >= dnext))
+      while (tryDist >= dnext) {
       const VoxDyn& d = f.dyn[DI];
       raySpeed = d.dist - dist;
       dist = d.dist;
@@ -241,16 +215,14 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
         }
       }
       DI++;
-#if SFRT_VOX_VARIANT & 1
       dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf("");
-#endif
     }
 
     dist = tryDist;
     pos = tryPos;
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
-    const int32_t cell = cell_of(f, pix, piy, piz);
-    if (cell >= 0 && occupied(f, cell)) {  // hit a block (World.cpp:385)
+    uint32_t cell;
+    if (cell_hit(f, pix, piy, piz, cell)) {  // hit a block (World.cpp:385)
       const int16_t id = block_id(f, cell);
       uint32_t c;
       if (id < 0) {
@@ -346,7 +318,6 @@ __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f
   const int b = f.sub_row0 + ty * 8 + (lane >> 3);
   // Edge lanes trace a clamped duplicate pixel and store nothing (a divergent
   // branch around raycast() would make its wave-uniform choices divergent).
-  const bool in = a < f.sub_w && b < f.sub_row0 + f.sub_rows;
   const int ac = a < f.sub_w ? a : f.sub_w - 1;
   const int bc = b < f.sub_row0 + f.sub_rows ? b : f.sub_row0 + f.sub_rows - 1;
   uint32_t work = 0;
@@ -354,7 +325,11 @@ __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f
   const int j = f.ystart + bc * f.yadd;
   const V3 dir{f.col[3 * i], f.row[2 * j], f.col[3 * i + 1]};
   const uint32_t rgba = raycast(f, dir, f.row[2 * j + 1], f.col[3 * i + 2], work);
-  if (in) f.out[(long long)(b - f.sub_row0) * f.out_pitch + a] = rgba;
+  // The store's pixel from the lane id again (mbcnt, not threadIdx): kept live across
+  // raycast(), a, b and `in` were spilled to scratch (16 bytes per lane).
+  const int lane2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int a2 = tx * 8 + (lane2 & 7), r2 = ty * 8 + (lane2 >> 3);
+  if (a2 < f.sub_w && r2 < f.sub_rows) f.out[(long long)r2 * f.out_pitch + a2] = rgba;
   if (f.tile_cost) {
     // the tile's slowest ray, in DDA + shadow steps / 4 (the classes' scale)
     const uint32_t w = wave_max_u32(work);
