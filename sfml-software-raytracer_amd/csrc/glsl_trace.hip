@@ -105,8 +105,14 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
     const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
     const float s = (rx * rx + ry * ry) + rz * rz;
     const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
-    if (__builtin_amdgcn_ballot_w64(inside)) {
-      moved = true;
+    // A wave with no lane inside skips the body: every lane's tosurf would be +0 (the uniforms
+    // are bounded, so (...) is finite and >= 0) and pos + dir * +0 == pos unless a component
+    // is -0.0, which pos holds only if campos does (x + y == -0 needs both -0): then the body
+    // runs for every iteration (cam_negzero, host-set), as the shader does.  One update path,
+    // so the loop-carried position needs no register copies on the skipping iterations.
+    const uint64_t inside_mask = __builtin_amdgcn_ballot_w64(inside);  // scalar tests only
+    if ((inside_mask | (uint64_t)(uint32_t)f.cam_negzero) != 0) {
+      moved |= inside_mask != 0;
       const float cs = inside ? 1.0f : 0.0f;
       const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
       const float c = cs * s - w.rr;
@@ -115,14 +121,6 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
       py = py + dy * tosurf;
       pz = pz + dz * tosurf;
       total = total + tosurf;
-    } else if (f.cam_negzero) {
-      // No lane inside: tosurf = 0 * (...) * 0.5 == +0 for every lane (the
-      // uniforms are bounded, so (...) is finite and >= 0).  pos + dir * +0
-      // then only turns a -0.0 component into +0.0, and pos holds a -0.0 only
-      // if campos does (x + y == -0 needs both -0); total + +0 == total.
-      px = px + dx * 0.0f;
-      py = py + dy * 0.0f;
-      pz = pz + dz * 0.0f;
     }
     draw = inside ? k : draw;
     if (++k == f.sc) {
