@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <mutex>
+#include <algorithm>
 #include <vector>
 
 #include "sfrt.h"
@@ -212,6 +213,7 @@ struct sfrt_voxel {
     f.row = (const float*)(d + b_col);
     f.blocks = d_blocks;
     f.nx = nx; f.ny = ny; f.nz = nz;
+    f.grid_bytes = (uint32_t)std::min<uint64_t>((uint64_t)nx * ny * nz * 2u, 0xffffffffu);
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
       f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};
       f.dyn_tex[k] = {dyn_tex[k].d, dyn_tex[k].w, dyn_tex[k].h};

@@ -59,6 +59,7 @@ struct VoxFrame {
   const float* row;                         // per row j: dir.y, yscale
   const int16_t* blocks;                    // dense [nx][ny][nz], textureID or kVoxEmpty
   int32_t nx, ny, nz;
+  uint32_t grid_bytes;                      // nx * ny * nz * 2, at most 2^32 - 1 (buffer range)
   VoxTex tex[kVoxSlots];
   VoxTex dyn_tex[kVoxSlots];
   uint32_t colors[kVoxSlots];               // RGBA8 packed

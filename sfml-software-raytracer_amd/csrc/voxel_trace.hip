@@ -41,27 +41,26 @@ struct V3 {
 // blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff the key is
 // non-negative and decodes to an occupied cell of the dense grid.  Branch-free: a negative key
 // has cx = key >> 20 (logical) >= 2048 >= nx, so three unsigned compares decide validity alone;
-// the index (cx * ny + cy) * nz + cz is computed for every lane and an invalid lane reads cell 0
-// (in bounds) -- no exec-mask branches around the per-step lookup (profiles/ab/r4_ab1).
+// the index (cx * ny + cy) * nz + cz is computed for every lane and read through a buffer
+// resource over the grid (32-bit offset, hardware range check: an invalid lane's offset may
+// point anywhere and reads harmlessly) -- no exec-mask branches or 64-bit address arithmetic
+// around the per-step lookup (profiles/ab/r4_ab1, r4_ab4).
 // nx <= kVoxMaxX, ny <= kVoxMaxY, nz <= kVoxMaxZ (voxel_trace.h, static_asserts there): for a
 // valid cell every factor is below 2^24 and the index below 2^31, so two full-rate
 // v_mad_u32_u24 and a 32-bit byte offset are exact (left alone, the compiler turns the first
-// into a quarter-rate v_mad_u64_u32).  `cell` is the index for block_id when the cell is hit.
+// into a quarter-rate v_mad_u64_u32).  `id` is the cell's texture id when the cell is hit.
 __device__ __forceinline__ bool cell_hit(const VoxFrame& f, int32_t x, int32_t y, int32_t z,
-                                         uint32_t& cell) {
+                                         int16_t& id) {
   const uint32_t key = ((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z;
   const uint32_t cx = key >> 20, cy = (key >> 10) & 1023u, cz = key & 1023u;
   const bool valid = (cx < (uint32_t)f.nx) & (cy < (uint32_t)f.ny) & (cz < (uint32_t)f.nz);
   uint32_t c;
   __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(cx), "s"((uint32_t)f.ny), "v"(cy));
   __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(c), "s"((uint32_t)f.nz), "v"(cz));
-  c = valid ? c : 0u;
-  cell = c;
-  return valid & (*(const int16_t*)((const char*)f.blocks + c * 2u) != kVoxEmpty);
-}
-
-__device__ __forceinline__ int16_t block_id(const VoxFrame& f, uint32_t c) {
-  return *(const int16_t*)((const char*)f.blocks + c * 2u);
+  const __amdgpu_buffer_rsrc_t grid =
+      __builtin_amdgcn_make_buffer_rsrc((void*)f.blocks, (short)0, (int)f.grid_bytes, 0x00020000);
+  id = (int16_t)__builtin_amdgcn_raw_buffer_load_b16(grid, (int)(c * 2u), 0, 0);
+  return valid & (id != kVoxEmpty);
 }
 
 __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, uint32_t x,
@@ -119,8 +118,8 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
     work++;
-    uint32_t cell;
-    if (cell_hit(f, pix, piy, piz, cell)) return false;
+    int16_t id;
+    if (cell_hit(f, pix, piy, piz, id)) return false;
     const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
     const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
     const float c = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
@@ -152,7 +151,10 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   float dist = 0.0f;
   V3 pos = cam;
   int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
-  V3 tryPos = pos;
+  // The reference's tryPos (World.cpp:318) equals pos at the top of every step (pos = tryPos
+  // ends each step), so the step advances pos in place after the billboard loop, which works
+  // on copies of pos and dist (the reference moves both there and then overwrites them with
+  // tryPos / tryDist): no second position carried around the loop and copied back each step.
   const float dirxadd = dir.x > 0 ? 1.0f : 0.0f, diryadd = dir.y > 0 ? 1.0f : 0.0f,
               dirzadd = dir.z > 0 ? 1.0f : 0.0f;
   float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
@@ -162,7 +164,6 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
               yz = RECIP ? 1.0f / lz : 0.0f;
   int DI = 0;
   float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // next billboard; NaN: never >=
-  float raySpeed = 0.0f;
   int colRay = 0;
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
     work++;
@@ -173,11 +174,8 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     // (as branches the compiler built an exec-mask diamond with ~12 scalar instructions)
     const bool ax = (xray <= yray) & (xray <= zray);
     const bool ay = !ax & (yray <= xray) & (yray <= zray);
-    raySpeed = ax ? xray : (ay ? yray : zray);
+    const float raySpeed = ax ? xray : (ay ? yray : zray);
     const float rs2 = raySpeed + 0.002f;
-    tryPos.x += dir.x * (ax ? rs2 : raySpeed);
-    tryPos.y += dir.y * (ay ? rs2 : raySpeed);
-    tryPos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
     colRay = ax ? 1 : (ay ? 2 : 3);
     const float tryDist = dist + raySpeed;
 
@@ -185,20 +183,22 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     // the next billboard's distance is held in a register (NaN past the last), so the test
     // reads no memory on the steps that pass no billboard (nearly all; it was a dependent
     // global load at every step), and a wave whose lanes all pass none skips the loop
-    if (__builtin_amdgcn_ballot_w64(tryDist >= dnext))
+    if (__builtin_amdgcn_ballot_w64(tryDist >= dnext)) {
+      V3 bp = pos;
+      float bdist = dist;
       while (tryDist >= dnext) {
       const VoxDyn& d = f.dyn[DI];
-      raySpeed = d.dist - dist;
-      dist = d.dist;
-      pos.x = pos.x + dir.x * raySpeed;
-      pos.y = pos.y + dir.y * raySpeed;
-      pos.z = pos.z + dir.z * raySpeed;
-      const float to = d.py - pos.y;
+      const float bs = d.dist - bdist;
+      bdist = d.dist;
+      bp.x = bp.x + dir.x * bs;
+      bp.y = bp.y + dir.y * bs;
+      bp.z = bp.z + dir.z * bs;
+      const float to = d.py - bp.y;
       const float sizey = d.sy * yscale;
       if (fabsf(to) < sizey) {
         float ang = d.atan_b - atan_dir;  // VAngleXZ(dir, VNormalizeXZ(d->pos - cam.pos))
         ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
-        ang = ang * dist;
+        ang = ang * bdist;
         const VoxTex& t = f.dyn_tex[d.tex];
         const float xf = (0.5f + ang / kPI * 0.5f / d.sx);
         if (xf > 0 && xf < 1) {
@@ -216,14 +216,16 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       }
       DI++;
       dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf("");
+      }
     }
 
     dist = tryDist;
-    pos = tryPos;
+    pos.x += dir.x * (ax ? rs2 : raySpeed);  // tryPos (World.cpp:330-350)
+    pos.y += dir.y * (ay ? rs2 : raySpeed);
+    pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
-    uint32_t cell;
-    if (cell_hit(f, pix, piy, piz, cell)) {  // hit a block (World.cpp:385)
-      const int16_t id = block_id(f, cell);
+    int16_t id;
+    if (cell_hit(f, pix, piy, piz, id)) {  // hit a block (World.cpp:385)
       uint32_t c;
       if (id < 0) {
         c = f.colors[-id];
