@@ -143,6 +143,66 @@ __device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
   return lraycast_t<true>(f, pos, dir, maxDist, work);
 }
 
+// The hit block of World::Raycast (World.cpp:385-450): texel of the face the step crossed,
+// light from every light source with shadow rays.  `dist` is the step's tryDist.
+template <bool RECIP>
+__device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t pix, int32_t piy,
+                                              int32_t piz, int colRay, float sx, float sy,
+                                              float sz, float dist, int16_t id, uint32_t& work) {
+  uint32_t c;
+  if (id < 0) {
+    c = f.colors[-id];
+  } else {
+    const VoxTex& t = f.tex[id];
+    const float tw = (float)(uint32_t)t.w, th = (float)(uint32_t)t.h;
+    if (colRay == 1) {
+      c = texel(f, t, to_u32(tw * (pos.z - (float)piz)), to_u32(th * (pos.y - (float)piy)));
+      pos.x += sx * 0.01f;  // get it off the wall
+      sy = 0.0f;
+      sz = 0.0f;
+    } else if (colRay == 2) {
+      c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.z - (float)piz)));
+      pos.y += sy * 0.01f;
+      sx = 0.0f;
+      sz = 0.0f;
+    } else {
+      c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.y - (float)piy)));
+      pos.z += sz * 0.01f;
+      sx = 0.0f;
+      sy = 0.0f;
+    }
+  }
+  const float l0 = 0.05f / dist - dist * 0.0001f;
+  float litr = l0 < 0.0f ? 0.0f : l0;
+  float litg = litr, litb = litr;
+  for (int j = 0; j < f.nlights; j++) {
+    const VoxLight L = light_at(f.lights, j);
+    const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
+    float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
+    float add = (L.intensity / dd - dd * 0.002f);
+    if (add > 0) {
+      float nx = L.px - pos.x, ny = L.py - pos.y, nz = L.pz - pos.z;
+      add *= ((nx * sx + ny * sy + nz * sz) * 0.7f + 0.3f);
+      if (add > 0) {
+        bool lit = true;
+        if (L.shadows && dist < f.shadow_distance) {
+          dd = __builtin_sqrtf(nx * nx + ny * ny + nz * nz);  // VLength
+          nx = nx / dd; ny = ny / dd; nz = nz / dd;
+          lit = lraycast(f, pos, V3{nx, ny, nz}, dd, work);
+        }
+        if (lit) {
+          litr += add * L.r;
+          litg += add * L.g;
+          litb += add * L.b;
+        }
+      }
+    }
+  }
+  return pack(to_u8(min255((float)(c & 0xffu) * litr)),
+              to_u8(min255((float)((c >> 8) & 0xffu) * litg)),
+              to_u8(min255((float)((c >> 16) & 0xffu) * litb)), c >> 24);
+}
+
 // World::Raycast, World.cpp:302-453.
 template <bool RECIP>
 __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
@@ -157,8 +217,8 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   // tryPos / tryDist): no second position carried around the loop and copied back each step.
   const float dirxadd = dir.x > 0 ? 1.0f : 0.0f, diryadd = dir.y > 0 ? 1.0f : 0.0f,
               dirzadd = dir.z > 0 ? 1.0f : 0.0f;
-  float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
-        sz = dir.z > 0 ? -1.0f : 1.0f;   // dir*sign (short, exact as float)
+  const float sx = dir.x > 0 ? -1.0f : 1.0f, sy = dir.y > 0 ? -1.0f : 1.0f,
+              sz = dir.z > 0 ? -1.0f : 1.0f;   // dir*sign (short, exact as float)
   const float lx = fabsf(dir.x), ly = fabsf(dir.y), lz = fabsf(dir.z);
   const float yx = RECIP ? 1.0f / lx : 0.0f, yy = RECIP ? 1.0f / ly : 0.0f,
               yz = RECIP ? 1.0f / lz : 0.0f;
@@ -225,60 +285,8 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
     int16_t id;
-    if (cell_hit(f, pix, piy, piz, id)) {  // hit a block (World.cpp:385)
-      uint32_t c;
-      if (id < 0) {
-        c = f.colors[-id];
-      } else {
-        const VoxTex& t = f.tex[id];
-        const float tw = (float)(uint32_t)t.w, th = (float)(uint32_t)t.h;
-        if (colRay == 1) {
-          c = texel(f, t, to_u32(tw * (pos.z - (float)piz)), to_u32(th * (pos.y - (float)piy)));
-          pos.x += sx * 0.01f;  // get it off the wall
-          sy = 0.0f;
-          sz = 0.0f;
-        } else if (colRay == 2) {
-          c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.z - (float)piz)));
-          pos.y += sy * 0.01f;
-          sx = 0.0f;
-          sz = 0.0f;
-        } else {
-          c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.y - (float)piy)));
-          pos.z += sz * 0.01f;
-          sx = 0.0f;
-          sy = 0.0f;
-        }
-      }
-      const float l0 = 0.05f / dist - dist * 0.0001f;
-      float litr = l0 < 0.0f ? 0.0f : l0;
-      float litg = litr, litb = litr;
-      for (int j = 0; j < f.nlights; j++) {
-        const VoxLight L = light_at(f.lights, j);
-        const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
-        float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
-        float add = (L.intensity / dd - dd * 0.002f);
-        if (add > 0) {
-          float nx = L.px - pos.x, ny = L.py - pos.y, nz = L.pz - pos.z;
-          add *= ((nx * sx + ny * sy + nz * sz) * 0.7f + 0.3f);
-          if (add > 0) {
-            bool lit = true;
-            if (L.shadows && tryDist < f.shadow_distance) {
-              dd = __builtin_sqrtf(nx * nx + ny * ny + nz * nz);  // VLength
-              nx = nx / dd; ny = ny / dd; nz = nz / dd;
-              lit = lraycast(f, pos, V3{nx, ny, nz}, dd, work);
-            }
-            if (lit) {
-              litr += add * L.r;
-              litg += add * L.g;
-              litb += add * L.b;
-            }
-          }
-        }
-      }
-      return pack(to_u8(min255((float)(c & 0xffu) * litr)),
-                  to_u8(min255((float)((c >> 8) & 0xffu) * litg)),
-                  to_u8(min255((float)((c >> 16) & 0xffu) * litb)), c >> 24);
-    }
+    if (cell_hit(f, pix, piy, piz, id))  // hit a block (World.cpp:385)
+      return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist, id, work);
   }
   return pack(0, 0, 0, 255);  // sf::Color::Black
 }
