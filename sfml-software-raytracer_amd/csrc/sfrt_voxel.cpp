@@ -90,6 +90,11 @@ struct sfrt_voxel {
   TableSlot slots[kSlots];
   int next_slot = 0;
   int cur_slot = -1;
+  // The tables depend only on the size, the camera, the billboards and the lights: every
+  // setter of those bumps tables_version, and a launch whose tables are unchanged since the
+  // last staging reuses that slot (no host recomputation, no copy).
+  uint64_t tables_version = 1, staged_version = 0;
+  size_t staged_off[3] = {0, 0, 0};  // byte offsets of row | dyn | lights in the staged slot
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
@@ -133,6 +138,13 @@ struct sfrt_voxel {
     const float vOff = std::sin(cam.hrotation);
     const float hStart = cam.rotation - cam.fov_h / 2;
     const float hIncreaseBy = cam.fov_h / width;
+    if (staged_version == tables_version && cur_slot >= 0) {
+      TableSlot& t = slots[cur_slot];  // still holds this scene's tables; launched() re-marks it
+      const int rc = blocks_upload();  // first: fill_frame reads d_blocks
+      if (rc != SFRT_OK) return rc;
+      fill_frame(f, (uint8_t*)t.d, staged_off);
+      return SFRT_OK;
+    }
     std::vector<float> col((size_t)width * 3), row((size_t)height * 2);
     for (int i = 0; i < width; i++) {
       const float hray = (hStart + hIncreaseBy * i);
@@ -195,7 +207,17 @@ struct sfrt_voxel {
     HIP_TRY(hipMemcpyAsync(t.d, t.h, bytes, hipMemcpyHostToDevice, s));
     cur_slot = next_slot;
     next_slot = (next_slot + 1) % kSlots;
-    uint8_t* d = (uint8_t*)t.d;
+    staged_version = tables_version;
+    staged_off[0] = b_col;
+    staged_off[1] = b_col + b_row;
+    staged_off[2] = b_col + b_row + b_dyn;
+    const int rc = blocks_upload();  // first: fill_frame reads d_blocks
+    if (rc != SFRT_OK) return rc;
+    fill_frame(f, (uint8_t*)t.d, staged_off);
+    return SFRT_OK;
+  }
+
+  int blocks_upload() {
     if (blocks_dirty) {  // rare: launches on any stream may still read the old grid
       HIP_TRY(hipDeviceSynchronize());
       if (d_blocks_cap < blocks.size()) {
@@ -209,8 +231,14 @@ struct sfrt_voxel {
                         hipMemcpyHostToDevice));
       blocks_dirty = false;
     }
+    return SFRT_OK;
+  }
+
+  // The frame record's device pointers: the staged tables at d, the grid (blocks_upload()
+  // must have run: the kernel's buffer resource over d_blocks has no other guard).
+  void fill_frame(sfrt::VoxFrame& f, uint8_t* d, const size_t* off) {
     f.col = (const float*)d;
-    f.row = (const float*)(d + b_col);
+    f.row = (const float*)(d + off[0]);
     f.blocks = d_blocks;
     f.nx = nx; f.ny = ny; f.nz = nz;
     f.grid_bytes = (uint32_t)std::min<uint64_t>((uint64_t)nx * ny * nz * 2u, 0xffffffffu);
@@ -219,12 +247,11 @@ struct sfrt_voxel {
       f.dyn_tex[k] = {dyn_tex[k].d, dyn_tex[k].w, dyn_tex[k].h};
       f.colors[k] = colors[k];
     }
-    f.dyn = (const sfrt::VoxDyn*)(d + b_col + b_row);
+    f.dyn = (const sfrt::VoxDyn*)(d + off[1]);
     f.ndyn = (int)dyn.size();
-    f.lights = (const sfrt::VoxLight*)(d + b_col + b_row + b_dyn);
+    f.lights = (const sfrt::VoxLight*)(d + off[2]);
     f.nlights = (int)lights.size();
     f.status = d_status;
-    return SFRT_OK;
   }
 
   // Marks the current table slot busy until the work queued on s completes.
@@ -276,6 +303,7 @@ int sfrt_voxel_set_size(sfrt_voxel* v, int width, int height) {
   std::lock_guard<std::mutex> lk(v->mu);
   v->width = width;
   v->height = height;
+  v->tables_version++;
   return SFRT_OK;
 }
 
@@ -286,6 +314,7 @@ int sfrt_voxel_set_camera(sfrt_voxel* v, const sfrt_camera* cam) {
     if (!std::isfinite(c)) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   v->cam = *cam;
+  v->tables_version++;
   return SFRT_OK;
 }
 
@@ -344,6 +373,7 @@ int sfrt_voxel_set_dynamics(sfrt_voxel* v, const sfrt_dynamic* dyn, int count) {
     if (dyn[k].texture_id < 0 || dyn[k].texture_id >= sfrt::kVoxSlots) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   v->dyn.assign(dyn, dyn + count);
+  v->tables_version++;
   return SFRT_OK;
 }
 
@@ -351,6 +381,7 @@ int sfrt_voxel_set_lights(sfrt_voxel* v, const sfrt_light* lights, int count) {
   if (!v || count < 0 || (count > 0 && !lights)) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   v->lights.assign(lights, lights + count);
+  v->tables_version++;
   return SFRT_OK;
 }
 

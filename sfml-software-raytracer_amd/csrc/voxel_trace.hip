@@ -360,6 +360,11 @@ long long voxel_tile_key(const VoxFrame& f, long long* tiles) {
 int launch_voxel(const VoxFrame& f, void* stream) {
   long long tiles = 0;
   if (voxel_tile_key(f, &tiles) == 0) return 0;
+  // the kernel reads the grid through a buffer resource over f.blocks and the tables
+  // unguarded: refuse a record whose device pointers were not filled
+  if (!f.blocks || f.grid_bytes == 0 || !f.col || !f.row || !f.out || !f.status ||
+      (f.ndyn > 0 && !f.dyn) || (f.nlights > 0 && !f.lights))
+    return -1;
   if (tiles > 0x7ffffffeLL) return -1;
   // row-major unless the host linked this launch into its tile-order chain
   hipLaunchKernelGGL(k_voxel_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,

@@ -150,3 +150,60 @@ def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
             o = oracle.VoxelOracle(vs.default_world(p, r, hr), width, height, assets[0], assets[1],
                                    vs.COLORS)
             assert np.array_equal(full, o.render(host_threads())), k
+
+
+@pytest.mark.gpu
+def test_voxel_tables_restaged_after_every_setter(vworld, assets):
+    """The per-frame tables (columns, rows, billboards, lights) are staged once and reused
+    while nothing they depend on changes (sfrt_voxel.cpp tables_version): each setter alone --
+    camera, size, billboards, lights -- must be seen by the next frame, and a repeated frame
+    must equal the first.  Every frame is compared with the oracle of the scene it was given."""
+    import ctypes
+    import dataclasses
+    import sfrt
+    import torch
+    L = sfrt.lib()
+    stream = torch.cuda.Stream()
+
+    def frame(w, h):
+        b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        vworld.render_band(b.data_ptr(), w * 4, 0, h, stream.cuda_stream)
+        vworld.check(stream.cuda_stream)
+        return b.cpu().numpy().ravel()
+
+    def want(scene, w, h):
+        return oracle.VoxelOracle(scene, w, h, assets[0], assets[1], vs.COLORS).render(host_threads())
+
+    base = vs.default_world((20.5, 2.2, 40.5), 1.0, 0.1)
+    vworld.set_scene(base, 320, 180)
+    first = frame(320, 180)
+    assert np.array_equal(first, want(base, 320, 180))
+    assert np.array_equal(frame(320, 180), first)          # reused tables
+    # camera alone
+    moved = dataclasses.replace(base, cam_pos=(21.25, 2.2, 39.5), rotation=1.3)
+    cam = sfrt.Camera()
+    for k in range(3):
+        cam.pos[k] = float(moved.cam_pos[k])
+    cam.rotation, cam.hrotation = float(moved.rotation), float(moved.hrotation)
+    cam.fov_h, cam.fov_v = float(moved.fov_h), float(moved.fov_v)
+    assert L.sfrt_voxel_set_camera(vworld._h, ctypes.byref(cam)) == 0
+    assert np.array_equal(frame(320, 180), want(moved, 320, 180))
+    # size alone
+    assert L.sfrt_voxel_set_size(vworld._h, 200, 120) == 0
+    vworld.width, vworld.height = 200, 120
+    assert np.array_equal(frame(200, 120), want(moved, 200, 120))
+    # billboards alone: every sprite 0.4 closer to the camera's row of the list
+    dyn = moved.dyn.copy()
+    dyn["dist_to_camera"] = dyn["dist_to_camera"] * np.float32(0.5)
+    dyn["pos"][:, 1] = dyn["pos"][:, 1] + np.float32(0.25)
+    d = np.ascontiguousarray(dyn)
+    assert L.sfrt_voxel_set_dynamics(vworld._h, d.ctypes.data, d.shape[0]) == 0
+    moved = dataclasses.replace(moved, dyn=dyn)
+    assert np.array_equal(frame(200, 120), want(moved, 200, 120))
+    # lights alone: the first half of the active lights
+    lights = np.ascontiguousarray(moved.lights[: max(1, moved.lights.shape[0] // 2)])
+    assert L.sfrt_voxel_set_lights(vworld._h, lights.ctypes.data, lights.shape[0]) == 0
+    moved = dataclasses.replace(moved, lights=lights)
+    got = frame(200, 120)
+    assert np.array_equal(got, want(moved, 200, 120))
+    assert np.array_equal(frame(200, 120), got)
