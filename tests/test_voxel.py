@@ -207,3 +207,40 @@ def test_voxel_tables_restaged_after_every_setter(vworld, assets):
     got = frame(200, 120)
     assert np.array_equal(got, want(moved, 200, 120))
     assert np.array_equal(frame(200, 120), got)
+
+
+VOXEL_EDGE_CASES = [  # (width, height, cam_pos, rotation, hrotation, what)
+    # hray of column 0 is exactly 0: dir.x == 0, so those waves take the plain-division DDA
+    # (raycast_t<false>, lraycast_t<false>) instead of the reciprocal one
+    (320, 180, (15.5, 1.9, 15.5), float(vs.deg2rad(75)) / 2, 0.0, "axis_parallel_column"),
+    # outside the grid at negative coordinates: negative map keys, truncation toward zero and the
+    # reference's negative-fraction steps (World.cpp:330-350 with pos < 0)
+    (320, 180, (-1.5, 1.9, -1.5), 0.785, 0.0, "negative_coordinates"),
+    (320, 180, (-3.5, 4.5, 20.5), 1.5708, 0.0, "negative_x_facing_wall"),
+    # above the grid looking down: cells with y >= ny, rays entering through the ceiling layer
+    (320, 180, (50.5, 11.5, 50.5), 0.3, -1.2, "above_the_grid"),
+    (320, 180, (50.5, 10.25, 50.5), 0.3, -0.9, "just_above_the_ceiling"),
+    # integer camera position: every fraction starts at 0
+    (320, 180, (16.0, 2.0, 16.0), 1.0, 0.2, "integer_position"),
+    # looking straight along the floor far away: long DDA walks up to maxiter
+    (320, 180, (1.5, 0.5, 1.5), 0.785398, 0.0, "long_walks"),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", VOXEL_EDGE_CASES, ids=lambda c: c[-1])
+def test_voxel_gpu_edge_poses_match_oracle(vworld, assets, case):
+    """Poses that reach the DDA's rarely taken paths, byte for byte against the restatement
+    (oracle/voxelworld_oracle.c).  Reference: World::Raycast / LRaycast, World.cpp:302-491."""
+    w, h, p, r, hr, _ = case
+    scene = vs.default_world(p, r, hr)
+    o = oracle.VoxelOracle(scene, w, h, assets[0], assets[1], vs.COLORS)
+    vworld.set_scene(scene, w, h)
+    got = vworld.render()
+    want = o.render(host_threads())
+    g, wv = got.reshape(-1, 4), want.reshape(-1, 4)
+    bad = np.nonzero(np.any(g != wv, axis=1))[0]
+    assert bad.size == 0, (f"{bad.size} pixels differ, first ({bad[0] % w}, {bad[0] // w}): "
+                           f"gpu={g[bad[0]]} oracle={wv[bad[0]]}")
+    # the frame is not trivially empty: some pixel is not the background
+    assert len(np.unique(g, axis=0)) > 4
