@@ -28,7 +28,7 @@ struct GlslWall {                      // spheres[0 .. sphereCount)
 
 struct GlslBall {                      // spheres[sphereCount .. allSpheresCount)
   float x, y, z, r;
-  float r_skip;                        // r when r >= 0 (the march's dominance test), else NaN
+  float r_skip;                        // RU(r * (1+6e-6)) when r >= 0 (the march's dominance test), else NaN
   float pad0, pad1, pad2;
 };
 

@@ -72,6 +72,10 @@ __device__ __forceinline__ T ld(const_ptr<T> p, int i) {
   return v;
 }
 
+// The march's dominance-test bounds: RU(1.00001f * (1 + 6e-6)) and RU(1e-4f * (1 + 6e-6)); the
+// host inflates r_skip by the same (1 + 6e-6), rounding up (sfrt_glsl.cpp).
+constexpr float kThrMul = 0x1.00010ep+0f, kThrAdd = 0x1.a36ed4p-14f;
+
 __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall> walls,
                                          const_ptr<GlslBall> balls, int i, int row,
                                          uint32_t& work, bool store = true) {
@@ -147,21 +151,24 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
     closest = 0;
     float shortest = 9999999.0f;
     snx = sny = snz = 0.0f;
-    // Dominance threshold t*(1+1e-5) + 1e-4, t = max(smooth + 0.5, shortest,
-    // 0.5); it only changes when a ball's body runs.
+    // Dominance threshold (t*(1+1e-5) + 1e-4)*(1+6e-6), t = max(smooth + 0.5, shortest, 0.5),
+    // rounded up (kThrMul, kThrAdd); it only changes when a ball's body runs.
     float thr = 1e30f;
     for (int k = 0; k < nballs; k++) {
       const GlslBall b = ld(balls, k);
       const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
-      const float ss = (ox * ox + oy * oy) + oz * oz;
       // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
       // margin), polsmin returns smooth, closest/shortest keep their values and
       // normalFactor == 1, so the body changes nothing (smoothNormal at most
       // flips the sign of a zero component, which no output depends on).
-      // Tested on the squared length with relative margins.
+      // The test is ours, not the shader's: the squared length by two fmas and both bounds
+      // inflated by (1+6e-6) (r_skip on the host, thr here), which implies the round-3 test
+      // ss >= (r + t*(1+1e-5) + 1e-4)^2 * (1+1e-5) on the shader's own ss.
+      const float ssf = __builtin_fmaf(ox, ox, __builtin_fmaf(oy, oy, oz * oz));
       const float bnd = b.r_skip + thr;
-      const bool dominated = ss >= bnd * bnd * 1.00001f;
+      const bool dominated = ssf >= bnd * bnd;
       if (!__builtin_amdgcn_ballot_w64(!dominated)) continue;
+      const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100
       const float other = sqrt_cr(ss) - b.r;
       const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
       smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
@@ -171,7 +178,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
       snx = nf * snx - (1.0f - nf) * ox;
       sny = nf * sny - (1.0f - nf) * oy;
       snz = nf * snz - (1.0f - nf) * oz;
-      thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * 1.00001f + 1e-4f;
+      thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
     }
     ball_dist += smooth + 0.01f;
   }

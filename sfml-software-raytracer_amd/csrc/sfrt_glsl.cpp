@@ -214,7 +214,10 @@ struct sfrt_glsl {
     std::vector<sfrt::GlslBall> balls(nb > 0 ? nb : 1);
     for (int k = 0; k < nb; k++) {
       const float* S = v.spheres[sc + k];
-      balls[k] = {S[0], S[1], S[2], S[3], S[3] >= 0.0f ? S[3] : NAN, 0.0f, 0.0f, 0.0f};
+      // r_skip: r * (1 + 6e-6) rounded up, the dominance test's inflated radius (glsl_trace.hip
+      // kThrMul); NaN for r < 0 or NaN, so such a ball is never skipped
+      const float rs = S[3] >= 0.0f ? std::nextafter(S[3] * 0x1.000065p+0f, INFINITY) : NAN;
+      balls[k] = {S[0], S[1], S[2], S[3], rs, 0.0f, 0.0f, 0.0f};
     }
     std::vector<sfrt::GlslPair> pairs(lc * ns > 0 ? lc * ns : 1);
     for (int li = 0; li < lc; li++)

@@ -360,3 +360,44 @@ def test_gpu_adaptive_tile_order_same_bytes(shader, floor):
         assert np.array_equal(got, want), (k, first_diff(got, want, w))
         if k in (3, 10):
             assert np.array_equal(full, oracle.GlslOracle(u, *floor).render(w, h, host_threads())), k
+
+
+def test_march_dominance_test_implies_round3_test():
+    """glsl_trace.hip's dominance test (two fmas, bounds inflated by (1+6e-6) and rounded up:
+    kThrMul, kThrAdd, the host's r_skip) implies the round-3 test it replaced,
+    ss >= (r + t*(1+1e-5) + 1e-4)^2 * 1.00001f on the shader's own ss, whose sufficiency for
+    skipping a ball exactly is argued in DESIGN.md 5c.  binary32 emulated in numpy (products of
+    two binary32 values are exact in binary64; fma = one rounding of the exact sum, here a
+    binary64 sum rounded once more, good to far below the 1e-6 slack).  Borderline samples sit
+    within 1e-5 of the new test's threshold."""
+    f32 = np.float32
+    rng = np.random.default_rng(7)
+    n = 400_000
+    r = (rng.random(n) * 40.0).astype(f32)
+    r[: n // 10] = 0.0
+    t = (np.float64(0.5) + rng.random(n) * 60.0).astype(f32)      # max(smooth+0.5, shortest, 0.5)
+    k_mul, k_add, k_r = f32(float.fromhex("0x1.00010ep+0")), f32(float.fromhex("0x1.a36ed4p-14")), \
+        f32(float.fromhex("0x1.000065p+0"))
+    r_skip = np.nextafter((r * k_r).astype(f32), f32(np.inf))
+    thr_new = ((t * k_mul).astype(f32) + k_add).astype(f32)
+    thr_old = ((t * f32(1.00001)).astype(f32) + f32(1e-4)).astype(f32)
+    bnd_new = (r_skip + thr_new).astype(f32)
+    lim_new = (bnd_new * bnd_new).astype(f32)
+    bnd_old = (r + thr_old).astype(f32)
+    lim_old = ((bnd_old * bnd_old).astype(f32) * f32(1.00001)).astype(f32)
+    # points whose fma'd squared length lands around the new threshold (and some far off)
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1)[:, None]
+    scale = np.sqrt(lim_new.astype(np.float64)) * (1.0 + (rng.random(n) - 0.5) * 2e-5)
+    scale[: n // 20] *= 1.0 + rng.random(n // 20) * 3.0
+    o = (u * scale[:, None]).astype(f32)
+    ox, oy, oz = (o[:, i].astype(np.float64) for i in range(3))
+    inner = (oy * oy + (oz * oz).astype(f32).astype(np.float64)).astype(f32).astype(np.float64)
+    ssf = (ox * ox + inner).astype(f32)
+    ss = ((((ox * ox).astype(f32) + (oy * oy).astype(f32)).astype(f32)
+           + (oz * oz).astype(f32)).astype(f32))
+    new = ssf >= lim_new
+    old = ss >= lim_old
+    assert new.sum() > n // 4 and (~new).sum() > n // 4        # both outcomes well sampled
+    bad = np.nonzero(new & ~old)[0]
+    assert bad.size == 0, (bad.size, r[bad[0]], t[bad[0]], o[bad[0]])

@@ -62,9 +62,9 @@ ANCHORS = {
     "wall_inside_first": "moved |= inside_mask != 0;",
     "wall_inside_last": "total = total + tosurf;",
     "march_loop": "ball_dist += smooth + 0.01f;",
-    "ball_loop": "const bool dominated = ss >= bnd * bnd * 1.00001f;",
-    "ball_body_first": "const float other = sqrt_cr(ss) - b.r;",
-    "ball_body_last": "thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f)",
+    "ball_loop": "const bool dominated = ssf >= bnd * bnd;",
+    "ball_body_first": "const float ss = (ox * ox + oy * oy) + oz * oz;",
+    "ball_body_last": "thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul",
     "light_loop": "const float tlx = L.x - px, tly = L.y - py, tlz = L.z - pz;",
     "shadow_loop": "const float cosang = (-tnx * P.ux + -tny * P.uy) + -tnz * P.uz;",
     "shadow_body_first": "float sangle = sfrt_math::acosf(cosang);",
@@ -260,8 +260,9 @@ PATCHES = [
      "    cnt[2] += first_lane_here();\n    if (++steps > kGlslMarchCap) {"),
     ("      const GlslBall b = ld(balls, k);\n",
      "      const GlslBall b = ld(balls, k);\n      cnt[3] += first_lane_here();\n"),
-    ("      const float other = sqrt_cr(ss) - b.r;\n",
-     "      cnt[4] += first_lane_here();\n      const float other = sqrt_cr(ss) - b.r;\n"),
+    ("      const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100\n",
+     "      cnt[4] += first_lane_here();\n"
+     "      const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100\n"),
     ("    const GlslBall L = ld(balls, li);\n",
      "    const GlslBall L = ld(balls, li);\n    cnt[5] += first_lane_here();\n"),
     ("        const float cosang = (-tnx * P.ux + -tny * P.uy) + -tnz * P.uz;\n",
