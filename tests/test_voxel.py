@@ -231,14 +231,31 @@ VOXEL_EDGE_CASES = [  # (width, height, cam_pos, rotation, hrotation, what)
 @pytest.mark.parametrize("case", VOXEL_EDGE_CASES, ids=lambda c: c[-1])
 def test_voxel_gpu_edge_poses_match_oracle(vworld, assets, case):
     """Poses that reach the DDA's rarely taken paths, byte for byte against the restatement
-    (oracle/voxelworld_oracle.c).  Reference: World::Raycast / LRaycast, World.cpp:302-491."""
+    (oracle/voxelworld_oracle.c).  Reference: World::Raycast / LRaycast, World.cpp:302-491.
+    From negative coordinates a hit in cell 0 can come from a position in (-1, 0) (truncation
+    toward zero), whose negative fraction makes the reference read outside the texture (UB):
+    the restatement substitutes magenta and counts the read; the kernel substitutes the same
+    magenta and fails loudly (SFRT_E_TEXEL from check()), and its frame still equals the
+    restatement's."""
+    import sfrt
+    import torch
     w, h, p, r, hr, _ = case
     scene = vs.default_world(p, r, hr)
     o = oracle.VoxelOracle(scene, w, h, assets[0], assets[1], vs.COLORS)
-    vworld.set_scene(scene, w, h)
-    got = vworld.render()
+    before = oracle.VoxelOracle.bad_texel_reads()
     want = o.render(host_threads())
-    g, wv = got.reshape(-1, 4), want.reshape(-1, 4)
+    ub = oracle.VoxelOracle.bad_texel_reads() > before
+    vworld.set_scene(scene, w, h)
+    stream = torch.cuda.Stream()
+    dev = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+    vworld.render_band(dev.data_ptr(), w * 4, 0, h, stream.cuda_stream)
+    if ub:
+        with pytest.raises(sfrt.SfrtError) as e:
+            vworld.check(stream.cuda_stream)
+        assert e.value.code == -7, e.value   # SFRT_E_TEXEL
+    else:
+        vworld.check(stream.cuda_stream)
+    g, wv = dev.cpu().numpy().reshape(-1, 4), want.reshape(-1, 4)
     bad = np.nonzero(np.any(g != wv, axis=1))[0]
     assert bad.size == 0, (f"{bad.size} pixels differ, first ({bad[0] % w}, {bad[0] // w}): "
                            f"gpu={g[bad[0]]} oracle={wv[bad[0]]}")
