@@ -337,6 +337,10 @@ SFRT_API int sfrt_voxel_set_colors(sfrt_voxel* v, const uint8_t* rgba, int count
 /* `dyn` in list order (World.h:93) and `alights` in list order (World.h:95). */
 SFRT_API int sfrt_voxel_set_dynamics(sfrt_voxel* v, const sfrt_dynamic* dyn, int count);
 SFRT_API int sfrt_voxel_set_lights(sfrt_voxel* v, const sfrt_light* lights, int count);
+/* The smallest squared distance dd >= 0 at which a light of this intensity adds nothing,
+ * `intensity / dd - dd * 0.002f <= 0` in binary32 (World.cpp:425-426); 0 when no dd passes.
+ * The kernel skips a light for a wave none of whose hit points is that close. */
+SFRT_API float sfrt_voxel_light_dd_pass(float intensity);
 /* World::UpdateImage into the caller's host RGBA8 frame; only addressed pixels written. */
 SFRT_API int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd, int xstart,
                                      int xadd);

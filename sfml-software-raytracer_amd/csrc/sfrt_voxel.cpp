@@ -30,6 +30,31 @@ namespace {
 
 constexpr float kPI = 3.1415926535f;  // World.h:5
 
+// The light's contribution test of World::Raycast, `intensity / dd - dd * 0.002f > 0`
+// (World.cpp:425-426), for a squared distance dd >= 0: true for dd below a threshold and false
+// from it on (intensity / dd never increases with dd, dd * 0.002f never decreases, and each
+// rounds monotonically), so the smallest non-negative float where it is false is found by
+// bisection over the bit patterns of [+0, +inf].  The kernel skips a light for a wave none of
+// whose lanes has dd below it (VoxLight::dd_pass).
+static bool light_adds(float intensity, float dd) {
+  volatile float q = intensity / dd;   // binary32, correctly rounded (no contraction: FLAGS)
+  volatile float p = dd * 0.002f;
+  return q - p > 0.0f;
+}
+float light_dd_pass(float intensity) {
+  uint32_t lo = 0u, hi = 0x7f800000u;  // light_adds(+inf) is false for every intensity
+  if (!light_adds(intensity, 0.0f)) return 0.0f;
+  while (hi - lo > 1u) {               // invariant: adds at lo, not at hi
+    const uint32_t mid = lo + (hi - lo) / 2u;
+    float m;
+    std::memcpy(&m, &mid, 4);
+    if (light_adds(intensity, m)) lo = mid; else hi = mid;
+  }
+  float t;
+  std::memcpy(&t, &hi, 4);
+  return t;
+}
+
 // float -> unsigned as the reference's x86-64 build converts it.
 uint32_t to_u32(float f) {
   if (!(f > -9.2233720368547758e18f && f < 9.2233720368547758e18f)) return 0u;
@@ -177,7 +202,8 @@ struct sfrt_voxel {
     std::vector<sfrt::VoxLight> vl(lights.size());
     for (size_t k = 0; k < lights.size(); k++) {
       const sfrt_light& L = lights[k];
-      vl[k] = {L.pos[0], L.pos[1], L.pos[2], L.intensity, L.r, L.g, L.b, L.shadows, 0};
+      vl[k] = {L.pos[0], L.pos[1], L.pos[2], L.intensity, L.r, L.g, L.b, L.shadows,
+               light_dd_pass(L.intensity)};
     }
     // one blob per launch: col | row | dyn | lights, 16-byte aligned parts
     auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
@@ -376,6 +402,8 @@ int sfrt_voxel_set_dynamics(sfrt_voxel* v, const sfrt_dynamic* dyn, int count) {
   v->tables_version++;
   return SFRT_OK;
 }
+
+float sfrt_voxel_light_dd_pass(float intensity) { return light_dd_pass(intensity); }
 
 int sfrt_voxel_set_lights(sfrt_voxel* v, const sfrt_light* lights, int count) {
   if (!v || count < 0 || (count > 0 && !lights)) return SFRT_E_INVALID;

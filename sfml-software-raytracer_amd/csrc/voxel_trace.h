@@ -41,7 +41,10 @@ struct VoxLight {                           // struct Light (World.h:40-47)
   float px, py, pz;
   float intensity, r, g, b;
   int32_t shadows;
-  int32_t pad;
+  // Squared distances dd >= dd_pass have intensity / dd - dd * 0.002f <= 0 in binary32
+  // (World.cpp:425-426: the light adds nothing there): the smallest such float, found on the host
+  // by bisection over the bit patterns (the test is monotone in dd); 0 when no dd passes.
+  float dd_pass;
 };
 
 struct VoxTex {

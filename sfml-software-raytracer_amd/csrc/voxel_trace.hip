@@ -179,6 +179,11 @@ __device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t
     const VoxLight L = light_at(f.lights, j);
     const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
     float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
+#if SFRT_VOX_EXP & 2
+    // dd >= dd_pass: the light adds nothing (host threshold, exact); a wave none of whose lanes
+    // is that close skips the light's division and the rest
+    if (!__builtin_amdgcn_ballot_w64(dd < L.dd_pass)) continue;
+#endif
     float add = (L.intensity / dd - dd * 0.002f);
     if (add > 0) {
       float nx = L.px - pos.x, ny = L.py - pos.y, nz = L.pz - pos.z;
@@ -225,6 +230,14 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   int DI = 0;
   float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // next billboard; NaN: never >=
   int colRay = 0;
+#if SFRT_VOX_EXP & 1
+  // Shading after the loop: a lane that hits stops stepping and the wave shades all its hit
+  // lanes once, after the last lane has stopped (inside the loop the light loop and its shadow
+  // rays ran once per distinct hit step of the wave).
+  bool hit = false;
+  int16_t hid = 0;
+  uint32_t early = 0u;
+#endif
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
     work++;
     const float xray = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
@@ -268,9 +281,16 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
           y = y < 0 ? 0 : y;
           const uint32_t c = texel(f, t, (uint32_t)x, (uint32_t)y);
           if ((c >> 24) > 127u) {
+#if SFRT_VOX_EXP & 1
+            early = pack(to_u8(min255((float)(c & 0xffu) * d.r)),
+                         to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
+                         to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
+            goto done;
+#else
             return pack(to_u8(min255((float)(c & 0xffu) * d.r)),
                         to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
                         to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
+#endif
           }
         }
       }
@@ -285,10 +305,23 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
     int16_t id;
+#if SFRT_VOX_EXP & 1
+    if (cell_hit(f, pix, piy, piz, id)) {  // hit a block (World.cpp:385)
+      hit = true;
+      hid = id;
+      break;
+    }
+  }
+  if (hit) return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist, hid, work);
+  return pack(0, 0, 0, 255);  // sf::Color::Black
+done:
+  return early;
+#else
     if (cell_hit(f, pix, piy, piz, id))  // hit a block (World.cpp:385)
       return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist, id, work);
   }
   return pack(0, 0, 0, 255);  // sf::Color::Black
+#endif
 }
 
 __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,

@@ -42,7 +42,8 @@ ABI_SYMBOLS = (
     "sfrt_voxel_create", "sfrt_voxel_destroy", "sfrt_voxel_set_size", "sfrt_voxel_set_camera",
     "sfrt_voxel_set_view", "sfrt_voxel_set_blocks", "sfrt_voxel_load_texture",
     "sfrt_voxel_load_dyn_texture", "sfrt_voxel_set_colors", "sfrt_voxel_set_dynamics",
-    "sfrt_voxel_set_lights", "sfrt_voxel_update_image", "sfrt_voxel_render_band",
+    "sfrt_voxel_set_lights", "sfrt_voxel_light_dd_pass", "sfrt_voxel_update_image",
+    "sfrt_voxel_render_band",
     "sfrt_voxel_check", "sfrt_voxel_set_option",
     "sfrt_glsl_create", "sfrt_glsl_destroy", "sfrt_glsl_set_ground", "sfrt_glsl_set_uniforms",
     "sfrt_glsl_get_uniforms", "sfrt_glsl_set_uniform", "sfrt_glsl_set_uniform_int",
@@ -152,6 +153,7 @@ def lib() -> ctypes.CDLL:
         "sfrt_voxel_set_colors": ([vp, vp, c_int], c_int),
         "sfrt_voxel_set_dynamics": ([vp, vp, c_int], c_int),
         "sfrt_voxel_set_lights": ([vp, vp, c_int], c_int),
+        "sfrt_voxel_light_dd_pass": ([ctypes.c_float], ctypes.c_float),
         "sfrt_voxel_update_image": ([vp, vp, c_int, c_int, c_int, c_int], c_int),
         "sfrt_voxel_render_band": ([vp, vp, ctypes.c_int64, c_int, c_int, vp], c_int),
         "sfrt_voxel_check": ([vp, vp], c_int),

@@ -261,3 +261,29 @@ def test_voxel_gpu_edge_poses_match_oracle(vworld, assets, case):
                            f"gpu={g[bad[0]]} oracle={wv[bad[0]]}")
     # the frame is not trivially empty: some pixel is not the background
     assert len(np.unique(g, axis=0)) > 4
+
+
+def test_light_dd_pass_is_the_exact_threshold(built):
+    """sfrt_voxel_light_dd_pass (the kernel's per-wave light skip): the light's test
+    `intensity / dd - dd * 0.002f > 0` (World.cpp:425-426, binary32 as numpy evaluates it) holds
+    just below the threshold and fails at it and at a spread of larger dd.  CPU only."""
+    import sfrt
+    f32 = np.float32
+    L = sfrt.lib()
+    rng = np.random.default_rng(11)
+    intensities = np.concatenate([[2.0, 1.0, 0.5, 7.25, 1e-3, 1e6, 0.0, -1.0, np.inf],
+                                  rng.random(200) * 50.0]).astype(f32)
+
+    def adds(i, dd):
+        with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+            return bool(f32(f32(i / dd) - f32(dd * f32(0.002))) > f32(0))
+
+    for i in intensities:
+        t = f32(L.sfrt_voxel_light_dd_pass(float(i)))
+        if t == 0:
+            assert not adds(i, f32(0)), i
+            continue
+        assert not adds(i, t), (i, t)
+        assert adds(i, np.nextafter(t, f32(0))), (i, t)
+        for m in (1.0001, 1.5, 10.0, 1e6):
+            assert not adds(i, f32(t * f32(m))), (i, t, m)
