@@ -179,11 +179,9 @@ __device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t
     const VoxLight L = light_at(f.lights, j);
     const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
     float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
-#if SFRT_VOX_EXP & 2
     // dd >= dd_pass: the light adds nothing (host threshold, exact); a wave none of whose lanes
     // is that close skips the light's division and the rest
     if (!__builtin_amdgcn_ballot_w64(dd < L.dd_pass)) continue;
-#endif
     float add = (L.intensity / dd - dd * 0.002f);
     if (add > 0) {
       float nx = L.px - pos.x, ny = L.py - pos.y, nz = L.pz - pos.z;
@@ -230,14 +228,14 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   int DI = 0;
   float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // next billboard; NaN: never >=
   int colRay = 0;
-#if SFRT_VOX_EXP & 1
-  // Shading after the loop: a lane that hits stops stepping and the wave shades all its hit
-  // lanes once, after the last lane has stopped (inside the loop the light loop and its shadow
-  // rays ran once per distinct hit step of the wave).
+  // Shading after the loop: a lane that hits a block (or a billboard's opaque texel) stops
+  // stepping, and the wave shades all its hit lanes once, after its last lane has stopped.
+  // Shaded inside the loop, the light loop and its shadow rays ran once per distinct hit step
+  // of the wave with the lanes of that step only (profiles/ab/r4_ab7: 4K 299 -> 289 us; with
+  // the per-wave light skip 265 us).
   bool hit = false;
   int16_t hid = 0;
   uint32_t early = 0u;
-#endif
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
     work++;
     const float xray = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
@@ -281,16 +279,10 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
           y = y < 0 ? 0 : y;
           const uint32_t c = texel(f, t, (uint32_t)x, (uint32_t)y);
           if ((c >> 24) > 127u) {
-#if SFRT_VOX_EXP & 1
             early = pack(to_u8(min255((float)(c & 0xffu) * d.r)),
                          to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
                          to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
             goto done;
-#else
-            return pack(to_u8(min255((float)(c & 0xffu) * d.r)),
-                        to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
-                        to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
-#endif
           }
         }
       }
@@ -305,7 +297,6 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
     pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
     int16_t id;
-#if SFRT_VOX_EXP & 1
     if (cell_hit(f, pix, piy, piz, id)) {  // hit a block (World.cpp:385)
       hit = true;
       hid = id;
@@ -316,12 +307,6 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   return pack(0, 0, 0, 255);  // sf::Color::Black
 done:
   return early;
-#else
-    if (cell_hit(f, pix, piy, piz, id))  // hit a block (World.cpp:385)
-      return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist, id, work);
-  }
-  return pack(0, 0, 0, 255);  // sf::Color::Black
-#endif
 }
 
 __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
@@ -336,10 +321,9 @@ __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
 // The default: 8x8 tiles on a 1-D grid of one-wave workgroups in the adaptive
 // tile order (sfrt_device.h sort_tiles; workgroup 0 is the sorter when
 // prev_cost is set).
-// Seven waves per SIMD: at most 72 VGPRs (71 since the 24-bit cell index, no spill; round 2
-// with a 16-byte spill measured 3% faster than six waves at 76, profiles/ab/r2_ab15_voxel_waves.txt).
+// Eight waves per SIMD: 58 VGPRs since the shading left the DDA loop (72 before, seven waves).
 #ifndef SFRT_VOX_WAVES
-#define SFRT_VOX_WAVES 7
+#define SFRT_VOX_WAVES 8
 #endif
 __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f, int tiles_x, int ntiles) {
   const int lane = threadIdx.x & 63;
