@@ -1,7 +1,8 @@
 """Build-flag A/B of libsfrt.so builds, interleaved across processes, bytes checked.
 
     python tools/ab_libs.py --libs a.so,b.so,a.so@3 [--rounds 3] [--reps 40] [--cases 4k,4k_rot,...]
-(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE; lib#K sets SFRT_AB_KNOB=K for an
+(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE; lib^O sets SFRT_OPT_TILE_ORDER=O on the
+GLSL and voxel renderers; lib#K sets SFRT_AB_KNOB=K for an
 experimental build that reads it -- r2_ab28 read it as SFRT_SPLIT; the product reads none)
 
 Each round starts one process per library (SFRT_LIB=<lib>, the same sfrt.py), which
@@ -36,9 +37,12 @@ CASES = {
 
 def renderer(sfrt, scenes, sname, pose, width, height, rays):
     """An object with render_band(ptr, pitch, row0, rows, stream) / check(stream) for a case."""
+    order = os.environ.get("SFRT_AB_TILE_ORDER")  # "lib^O": the 8f renderers' tile order
     if sname.startswith("voxel:"):
         import voxel_scenes as vs
         v = sfrt.VoxelWorld(0)
+        if order is not None:
+            v.set_option(sfrt.SFRT_OPT_TILE_ORDER, int(order))
         tex, dyn = vs.load_textures()
         v.load_assets(tex, dyn, vs.COLORS)
         v.set_scene(vs.default_world(tuple(float(c) for c in sname[6:].split(",")), *pose),
@@ -47,6 +51,8 @@ def renderer(sfrt, scenes, sname, pose, width, height, rays):
     if sname == "glsl":
         import glsl_scenes as gs
         g = sfrt.GlslShader(0)
+        if order is not None:
+            g.set_option(sfrt.SFRT_OPT_TILE_ORDER, int(order))
         g.set_ground(*scenes.load_floor())
         g.set_uniforms(gs.default_uniforms(width, height, *pose))
 
@@ -140,11 +146,14 @@ def main():
     for rnd in range(a.rounds):
         for lib in libs:  # "path" or "path@R" (R = SFRT_OPT_RAYS_PER_LANE); "path!" = timing probe
             probe = lib.endswith("!")
-            spec, _, knob = lib.rstrip("!").partition("#")  # "#K": SFRT_AB_KNOB=K for an A/B build
+            spec, _, order = lib.rstrip("!").partition("^")  # "^O": 8f renderers' tile order
+            spec, _, knob = spec.partition("#")  # "#K": SFRT_AB_KNOB=K for an A/B build
             path, _, rays = spec.partition("@")
             env = dict(os.environ, SFRT_LIB=os.path.abspath(path))
             if knob:
                 env["SFRT_AB_KNOB"] = knob
+            if order:
+                env["SFRT_AB_TILE_ORDER"] = order
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "--libs", lib,
                                 "--cases", a.cases, "--reps", str(a.reps), "--rays", rays or "0"],
                                capture_output=True, text=True, env=env, timeout=600)
