@@ -80,7 +80,9 @@ def measured_traffic(pixels: int, kernel: str = "k_trace"):
         table = doc.get("per_launch_pixels", doc.get("per_grid_threads", {}))
         # the sphere kernel's steady-state launch has the tile-order sorter workgroup (+64 x R
         # pixels, R = 4, 3, 2 or 1 pixels per lane)
-        for extra in ((256, 192, 128, 64, 0) if kernel == "k_trace" else (0,)):
+        # (the GLSL renderer's ordered launch likewise, since round 4: one sorter workgroup of 64)
+        for extra in ((256, 192, 128, 64, 0) if kernel == "k_trace" else
+                      (64, 0) if kernel == "k_glsl" else (0,)):
             ent = table.get(str(pixels + extra))
             if ent:
                 return ent, os.path.relpath(path, ROOT)

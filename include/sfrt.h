@@ -401,9 +401,9 @@ SFRT_API int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int heigh
 /* rt.draw + rt.getTexture().copyToImage() into a host RGBA8 buffer (synchronous). */
 SFRT_API int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height);
 SFRT_API int sfrt_glsl_check(sfrt_glsl* g, void* hip_stream);
-/* SFRT_OPT_TILE_ORDER as for sfrt_world, off (0) by default here: sfrt_glsl_draw with 1
- * dispatches 8x8 tiles longest-first by the metaball-march steps of two frames back (same
- * bytes; measured 20-30% slower on the GLSL frames). */
+/* SFRT_OPT_TILE_ORDER as for sfrt_world, on (1) by default: sfrt_glsl_draw dispatches 8x8
+ * tiles longest-first by the metaball-march steps of two frames back (same bytes; 1-6 % faster
+ * on the round-4 kernel); 0 = row-major.  sfrt_glsl_draw_image is row-major. */
 SFRT_API int sfrt_glsl_set_option(sfrt_glsl* g, int option, int value);
 
 /* ======================================================================

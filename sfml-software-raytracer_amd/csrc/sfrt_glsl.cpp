@@ -92,7 +92,9 @@ struct sfrt_glsl {
   int device = 0;
   sfrt_glsl_uniforms u{};
   int ground_w = 0, ground_h = 0;
-  int tile_order_on = 0;               // SFRT_OPT_TILE_ORDER (sfrt_glsl_draw): off by default, slower here
+  // SFRT_OPT_TILE_ORDER (sfrt_glsl_draw): on by default since round 4 (1080p -6 %, 4K -1 %, also
+  // with the world moving every frame: profiles/ab/r4_ab9); draw_image stays row-major
+  int tile_order_on = 1;
   sfrt::TileSched sched;               // adaptive tile order (sfrt_sched.h)
   // device resources
   hipStream_t stream = nullptr;

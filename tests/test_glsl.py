@@ -342,7 +342,7 @@ def test_gpu_adaptive_tile_order_same_bytes(shader, floor):
     import sfrt
     stream = torch.cuda.Stream()
     frames = []
-    shader.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)  # off by default for the GLSL renderer
+    shader.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)  # the default since round 4
     with torch.cuda.stream(stream):
         for u, w, h, r0, rows in seq:
             shader.set_uniforms(u)
@@ -352,14 +352,17 @@ def test_gpu_adaptive_tile_order_same_bytes(shader, floor):
     shader.check(stream.cuda_stream)
     torch.cuda.synchronize()
     shader.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
-    for k, ((u, w, h, r0, rows), b) in enumerate(zip(seq, frames)):
-        full = draw(shader, u, w, h)
-        want = np.full(w * h * 4, 0xA5, dtype=np.uint8)
-        want[r0 * w * 4:(r0 + rows) * w * 4] = full[r0 * w * 4:(r0 + rows) * w * 4]
-        got = b.cpu().numpy().ravel()
-        assert np.array_equal(got, want), (k, first_diff(got, want, w))
-        if k in (3, 10):
-            assert np.array_equal(full, oracle.GlslOracle(u, *floor).render(w, h, host_threads())), k
+    try:
+        for k, ((u, w, h, r0, rows), b) in enumerate(zip(seq, frames)):
+            full = draw(shader, u, w, h)
+            want = np.full(w * h * 4, 0xA5, dtype=np.uint8)
+            want[r0 * w * 4:(r0 + rows) * w * 4] = full[r0 * w * 4:(r0 + rows) * w * 4]
+            got = b.cpu().numpy().ravel()
+            assert np.array_equal(got, want), (k, first_diff(got, want, w))
+            if k in (3, 10):
+                assert np.array_equal(full, oracle.GlslOracle(u, *floor).render(w, h, host_threads())), k
+    finally:
+        shader.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
 
 
 def test_march_dominance_test_implies_round3_test():

@@ -32,6 +32,10 @@ CASES = {
     "vox4k_rot": (3840, 2160, "voxel:47.5,1.5,60.1", (4.0, -0.3), False),
     "glsl1080": (1920, 1080, "glsl", (0.0, 0.0), False),
     "glsl4k": (3840, 2160, "glsl", (0.0, 0.0), False),
+    # the live loop's UpdateWorld every frame (Source.cpp:143-153): the world advanced one step
+    # per frame, the camera turning 0.004 rad per frame
+    "glsl4k_move": (3840, 2160, "glsl", (0.0, 0.0), True),
+    "glsl1080_move": (1920, 1080, "glsl", (0.0, 0.0), True),
 }
 
 
@@ -57,8 +61,15 @@ def renderer(sfrt, scenes, sname, pose, width, height, rays):
         g.set_uniforms(gs.default_uniforms(width, height, *pose))
 
         class Draw:
+            def __init__(self):
+                self.world = gs.ShaderWorld(0)
+
             def render_band(self, ptr, pitch, row0, rows, stream):
                 g.draw(ptr, width, height, pitch, row0, rows, stream)
+
+            def set_camera(self, _pos, rotation, hrotation):  # a moving case: one UpdateWorld
+                self.world.update_world()
+                g.set_uniforms(self.world.uniforms(width, height, rotation, hrotation))
 
             def check(self, stream):
                 g.check(stream)
@@ -91,20 +102,22 @@ def child(cases, reps, rays):
     for name in cases:
         width, height, sname, pose, turn = CASES[name]
         w, keep = renderer(sfrt, scenes, sname, pose, width, height, rays)
+        sc = None
         if w is None:
             w = sphere_world
             sc = scenes.SCENES[sname]().posed(*pose)
             w.set_scene(sc, width, height)
+        cam_pos = sc.cam_pos if sc is not None else None
         buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
         for k in range(20):  # warm-up (clock ramp, tile-order chain)
             if turn:
-                w.set_camera(sc.cam_pos, 0.004 * k, 0.0)
+                w.set_camera(cam_pos, 0.004 * k, 0.0)
             w.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(reps)]
         for k, (a, b) in enumerate(ev):
             if turn:
-                w.set_camera(sc.cam_pos, 0.004 * (20 + k), 0.0)
+                w.set_camera(cam_pos, 0.004 * (20 + k), 0.0)
             a.record(stream)
             w.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
             b.record(stream)
@@ -117,7 +130,7 @@ def child(cases, reps, rays):
         t0 = time.perf_counter()
         for k in range(reps):
             if turn:
-                w.set_camera(sc.cam_pos, 0.004 * (20 + reps + k), 0.0)
+                w.set_camera(cam_pos, 0.004 * (20 + reps + k), 0.0)
             w.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / reps

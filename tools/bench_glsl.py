@@ -25,9 +25,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--orders", default="0",
-                    help="SFRT_OPT_TILE_ORDER values (0 row-major = the default here, 1 adaptive; "
-                         "keys get /ordered)")
+    ap.add_argument("--orders", default="1",
+                    help="SFRT_OPT_TILE_ORDER values (1 adaptive = the library's default since "
+                         "round 4, 0 row-major; keys of 0 get /rowmajor)")
     ap.add_argument("--set", choices=("all", "bench"), default="all",
                     help="bench: only the two frames bench.py times (1080p and 4K, rot (0,0)), "
                          "one frame per launch size (rocprof summaries per launch size)")
@@ -49,8 +49,8 @@ def main():
             s.set_option(sfrt.SFRT_OPT_TILE_ORDER, order)
             r = time_one(s, buf, width, height, u, rot, frames, 0, args, stream, floor,
                          threads, oracle)
-            res.update({(k + ("/ordered" if order else "")): v for k, v in r.items()})
-        s.set_option(sfrt.SFRT_OPT_TILE_ORDER, 0)
+            res.update({(k + ("" if order else "/rowmajor")): v for k, v in r.items()})
+        s.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
     print(json.dumps(res, indent=1))
 
 
