@@ -116,6 +116,11 @@ struct sfrt_glsl {
   TableSlot slots[kSlots];
   int next_slot = 0;
   int cur_slot = -1;
+  // The tables depend only on the uniform block: every uniform setter bumps u_version, and a
+  // draw with the uniforms unchanged since the last staging reuses that slot (no host table
+  // build, no copy in front of the kernel).
+  uint64_t u_version = 1, staged_version = 0;
+  size_t staged_off[3] = {0, 0, 0};  // byte offsets of balls | pairs | mats in the staged slot
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
@@ -213,6 +218,10 @@ struct sfrt_glsl {
       }
       f.wall_start = j < sc ? j : 3 * sc;  // inside no wall: no lane ever moves
     }
+    if (staged_version == u_version && cur_slot >= 0) {  // launched() re-marks the slot
+      fill_tables(f, (uint8_t*)slots[cur_slot].d, staged_off);
+      return SFRT_OK;
+    }
     std::vector<sfrt::GlslBall> balls(nb > 0 ? nb : 1);
     for (int k = 0; k < nb; k++) {
       const float* S = v.spheres[sc + k];
@@ -278,11 +287,20 @@ struct sfrt_glsl {
     HIP_TRY(hipMemcpyAsync(t.d, blob, bytes, hipMemcpyHostToDevice, s));
     cur_slot = next_slot;
     next_slot = (next_slot + 1) % kSlots;
-    uint8_t* base = (uint8_t*)t.d;
+    staged_version = u_version;
+    staged_off[0] = bw;
+    staged_off[1] = bw + bb;
+    staged_off[2] = bw + bb + bp;
+    fill_tables(f, (uint8_t*)t.d, staged_off);
+    return SFRT_OK;
+  }
+
+  // The frame record's device pointers: the staged tables at base, the ground's mip chain.
+  void fill_tables(sfrt::GlslFrame& f, uint8_t* base, const size_t* off) {
     f.walls = (const sfrt::GlslWall*)base;
-    f.balls = (const sfrt::GlslBall*)(base + bw);
-    f.pairs = (const sfrt::GlslPair*)(base + bw + bb);
-    f.mats = (const sfrt::GlslMat*)(base + bw + bb + bp);
+    f.balls = (const sfrt::GlslBall*)(base + off[0]);
+    f.pairs = (const sfrt::GlslPair*)(base + off[1]);
+    f.mats = (const sfrt::GlslMat*)(base + off[2]);
     f.mip = d_mip;
     f.mip_levels = mip_levels;
     for (int k = 0; k < sfrt::kGlslMipLevels; k++) {
@@ -291,7 +309,6 @@ struct sfrt_glsl {
       f.mip_off[k] = mip_off[k];
     }
     f.status = d_status;
-    return SFRT_OK;
   }
 
   // Marks the current table slot busy until the work queued on s completes.
@@ -383,6 +400,7 @@ int sfrt_glsl_set_uniforms(sfrt_glsl* g, const sfrt_glsl_uniforms* u) {
   if (!g || !u) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(g->mu);
   g->u = *u;
+  g->u_version++;
   return SFRT_OK;
 }
 
@@ -414,6 +432,7 @@ int sfrt_glsl_set_uniform(sfrt_glsl* g, const char* name, const float* v, int n)
   }
   if (!dst || n != want) return SFRT_E_INVALID;
   std::memcpy(dst, v, sizeof(float) * n);
+  g->u_version++;
   return SFRT_OK;
 }
 
@@ -424,6 +443,7 @@ int sfrt_glsl_set_uniform_int(sfrt_glsl* g, const char* name, int value) {
   else if (!std::strcmp(name, "allSpheresCount")) g->u.all_spheres_count = value;
   else if (!std::strcmp(name, "lightCount")) g->u.light_count = value;
   else return SFRT_E_INVALID;
+  g->u_version++;
   return SFRT_OK;
 }
 

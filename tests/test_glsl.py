@@ -404,3 +404,42 @@ def test_march_dominance_test_implies_round3_test():
     assert new.sum() > n // 4 and (~new).sum() > n // 4        # both outcomes well sampled
     bad = np.nonzero(new & ~old)[0]
     assert bad.size == 0, (bad.size, r[bad[0]], t[bad[0]], o[bad[0]])
+
+
+@pytest.mark.gpu
+def test_gpu_tables_restaged_after_every_uniform_setter(shader, floor):
+    """The per-draw tables (walls, balls, light/shadow pairs, materials) are staged once and
+    reused while the uniforms do not change (sfrt_glsl.cpp u_version): a repeated draw equals
+    the first, and each setter alone -- the block, a float uniform by name, an int uniform by
+    name -- is seen by the next draw (compared with the oracle of the uniforms it was given)."""
+    import torch
+    w, h = 320, 180
+    stream = torch.cuda.Stream()
+
+    def frame():
+        b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        shader.draw(b.data_ptr(), w, h, w * 4, 0, h, stream.cuda_stream)
+        shader.check(stream.cuda_stream)
+        return b.cpu().numpy().ravel()
+
+    def want(u):
+        return oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+
+    u = gs.default_uniforms(w, h, 0.6, 0.1, frames=5)
+    shader.set_uniforms(u)
+    first = frame()
+    assert np.array_equal(first, want(u)), first_diff(first, want(u), w)
+    assert np.array_equal(frame(), first)                      # reused tables
+    u2 = np.array(u, copy=True)                                # a ball moved, by name
+    k = int(u2["sphere_count"]) + int(u2["light_count"])       # the first shadow ball
+    u2["spheres"][k, 0] += np.float32(0.75)
+    shader.set_uniform(f"spheres[{k}]", u2["spheres"][k])
+    got = frame()
+    assert np.array_equal(got, want(u2)), first_diff(got, want(u2), w)
+    u3 = np.array(u2, copy=True)                               # one light fewer, by name
+    u3["light_count"] = int(u3["light_count"]) - 1
+    shader.set_uniform("lightCount", int(u3["light_count"]))
+    got = frame()
+    assert np.array_equal(got, want(u3)), first_diff(got, want(u3), w)
+    shader.set_uniforms(u)                                     # the block again
+    assert np.array_equal(frame(), first)
