@@ -23,10 +23,11 @@ Blocks (fragment() in csrc/glsl_trace.hip, rayShader.frag lines):
   shadow_body    its soft-shadow body
   colour         colour, fog and the store (:153-158)
   rare           the keep_branch fallbacks (plain division, full sqrt lowering) that no wave of
-                 these frames takes (counted separately; excluded from the expected total)
+                 these frames takes, and the ordered kernel's tile sorter (one workgroup per
+                 launch) -- counted separately, excluded from the expected total
 
 `static` compiles the product source with -gline-tables-only (the ISA is checked identical to the
-release build's) and assigns each basic block of k_glsl (the row-major kernel bench.py times) to a
+release build's) and assigns each basic block of k_glsl_ordered (the kernel bench.py times) to a
 block by the ISA's loop structure and the source lines in it.  `build` copies the package's
 Makefile, csrc/ and include/ to sfml-software-raytracer_amd/build_glslprof/, patches the copy of
 glsl_trace.hip (never the product source) with per-block execution counters -- the first active
@@ -51,7 +52,9 @@ PKG = os.path.join(ROOT, "sfml-software-raytracer_amd")
 SRC = os.path.join(PKG, "csrc", "glsl_trace.hip")
 BASE = os.path.join(PKG, "build_glslprof")
 OUT = os.path.join(BASE, "pkg")  # BASE/include beside it: the Makefile's ../include
-KERNEL = "_ZN4sfrt12_GLOBAL__N_16k_glslENS_9GlslFrameE"
+# the ordered kernel sfrt_glsl_draw launches by default since round 4 (fragment() is the same
+# inlined body in k_glsl, the row-major kernel of draw_image)
+KERNEL = "_ZN4sfrt12_GLOBAL__N_114k_glsl_orderedENS_9GlslFrameEi"
 COUNTED = ["wall_test", "wall_inside", "march_step", "ball_test", "ball_body", "light",
            "shadow_test", "shadow_body"]
 ONCE = ["setup", "texture", "colour"]
@@ -163,6 +166,8 @@ def fragment_lines(co):
         for k in range(0, len(fr) - 1, 2):
             if fr[k] == "fragment":
                 line = int(fr[k + 1].split(":")[-2])
+            if fr[k].startswith("sort_tiles"):
+                line = -1  # the ordered kernel's tile sorter (workgroup 0)
         out.append((mn, line))
     return out
 
@@ -206,7 +211,7 @@ def static():
     def region(bl, line):
         h = bl["header"]
         inr = lambda a, z: line is not None and A[a] <= line <= A[z]
-        if bl["rare"]:
+        if bl["rare"] or line == -1:
             return "rare"
         if h == loops["wall_loop"]:
             return "wall_inside" if inr("wall_inside_first", "wall_inside_last") else "wall_test"
@@ -219,6 +224,8 @@ def static():
         if h == loops["light_loop"]:
             return "light"
         if h is not None:
+            if line is None:  # not fragment(): the tile sorter of the ordered kernel (workgroup 0)
+                return "rare"
             raise SystemExit(f"block {bl['name']} in an unexpected loop {h}")
         if line is None or line < sec["texture"]:
             return "setup"
@@ -363,7 +370,8 @@ def combine(counts_path, pmc_path):
                "predicted_valu_per_wave": round(tot, 1),
                "rare_fallback_valu_static": st["valu_per_execution"].get("rare", 0)}
         if pmc:
-            t = pmc.get("per_launch_pixels", pmc.get("per_grid_threads", {})).get(key)
+            tab = pmc.get("per_launch_pixels", pmc.get("per_grid_threads", {}))
+            t = tab.get(str(int(key) + 64)) or tab.get(key)  # the ordered launch: + the sorter
             if t:
                 row["pmc_valu_per_wave"] = round(t["SQ_INSTS_VALU"] / t["SQ_WAVES"], 1)
                 row["predicted_over_pmc"] = round(tot / row["pmc_valu_per_wave"], 4)
