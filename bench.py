@@ -342,8 +342,9 @@ def measure_frame(world, scene, width, height, rank, world_size, steps, warmup, 
     return {"n_gpus": world_size, "Mrays_per_s": round(width * height * steps / wall / 1e6, 2),
             "fps": round(steps / wall, 2), "ms_per_frame": round(wall / steps * 1e3, 4),
             "kernel_ms_rank0_band": round(kms, 4),
-            "hbm_frac_rank0_kernel": round(BYTES_PER_RAY * rays0 / (kms * 1e-3) / 1e9
-                                           / HBM_PEAK_GBS, 6),
+            # a small band (1080p over 8 ranks: 135 rows) can time at or below the event pair's
+            # own gap: hbm_frac() reports 0 there instead of dividing by it
+            "hbm_frac_rank0_kernel": hbm_frac(rays0, kms),
             "bands": bands, **(check or {})}
 
 
@@ -644,7 +645,7 @@ def main() -> None:
     result = None
     if rank == 0:
         rays_per_launch = WIDTH * rows
-        achieved = BYTES_PER_RAY * rays_per_launch / (kernel_ms * 1e-3) / 1e9
+        achieved = BYTES_PER_RAY * rays_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         result = {
             "metric": "Mrays/s (primary rays, full RGBA8 frames in HBM)",
             "value": round(value, 2),
@@ -689,7 +690,7 @@ def main() -> None:
         if meas:
             result["roofline"]["traffic"] = round(meas["hbm_bytes_per_launch"])
             result["roofline"]["traffic_source"] = src
-            if "SQ_INSTS_VALU" in meas:
+            if "SQ_INSTS_VALU" in meas and kernel_ms > 0:
                 rate = meas["SQ_INSTS_VALU"] / (kernel_ms * 1e-3)
                 result["valu_roofline"] = {
                     "achieved": round(rate / 1e12, 4), "peak": round(VALU_PEAK_WAVE_INSTS / 1e12, 4),
