@@ -14,7 +14,6 @@
 
 #include "glsl_trace.h"
 #include "sfrt_device.h"
-#include "sfrt_device.h"
 #include "sfrt_math.h"
 
 #pragma clang fp contract(off)

@@ -35,7 +35,7 @@ constexpr float kPI = 3.1415926535f;  // World.h:5
 // from it on (intensity / dd never increases with dd, dd * 0.002f never decreases, and each
 // rounds monotonically), so the smallest non-negative float where it is false is found by
 // bisection over the bit patterns of [+0, +inf].  The kernel skips a light for a wave none of
-// whose lanes has dd below it (VoxLight::dd_pass).
+// whose lanes has dd below it (VoxLight::dd_skip).
 static bool light_adds(float intensity, float dd) {
   volatile float q = intensity / dd;   // binary32, correctly rounded (no contraction: FLAGS)
   volatile float p = dd * 0.002f;
@@ -53,6 +53,34 @@ float light_dd_pass(float intensity) {
   float t;
   std::memcpy(&t, &hi, 4);
   return t;
+}
+
+// VoxLight::dd_skip from dd_pass: RU(dd_pass / (1 - 2^-20)), so that a squared distance
+// evaluated with fmas (relative error within 2^-20 of the reference's three products and two
+// sums, all terms non-negative) at or above it implies the reference's dd >= dd_pass.
+float light_dd_skip(float dd_pass) {
+  const double t = (double)dd_pass / (1.0 - 0x1.0p-20);
+  const float f = (float)t;
+  return (double)f >= t ? f : std::nextafter(f, INFINITY);
+}
+
+// The fast primary DDA's bound (VoxFrame::dda_qlim, voxel_trace.hip pos_i32).  At a position
+// with |p| < 2^30, a step of World::Raycast (World.cpp:330-350) divides a numerator in (-1, 2)
+// (dirXadd + sign * (p - (int)p)) by |d_k|, so |raySpeed| <= 2 (1 + 2^-23) / m with
+// m = min_k |d_k| (a negative fraction can make it negative), and moves axis j by at most
+// |d_j| (|raySpeed| + 0.002)(1 + 2^-21) <= 2.0001 X / m + 0.0021 X (X = max_k |d_k| <= xmax),
+// plus the add's rounding, <= 32 below 2^30.  So with Q = X / m, S = 2.001 Q + 0.003 xmax + 33
+// bounds one step and |cam| + (maxiter + 1) S <= 2^30 keeps every position of the walk below
+// 2^30, where the plain conversion equals to_i32 (only +2^31 and beyond and NaN differ).  The
+// kernel takes the fast DDA for a wave whose every lane has X <= qlim * m (the float product
+// rounds up at most 2^-24, absorbed by rounding qlim down by 2^-20); 0 disables it.
+float dda_qlim(const float cam[3], uint32_t maxiter, float xmax) {
+  const double p = std::max({std::fabs((double)cam[0]), std::fabs((double)cam[1]),
+                             std::fabs((double)cam[2])});
+  const double q = ((1073741824.0 - p) / ((double)maxiter + 1.0) - 33.0 - 0.003 * xmax) / 2.001;
+  if (!(q > 1.0) || !std::isfinite(xmax)) return 0.0f;
+  const float f = (float)(q * (1.0 - 0x1.0p-20));
+  return (double)f <= q * (1.0 - 0x1.0p-20) ? f : std::nextafter(f, 0.0f);
 }
 
 // float -> unsigned as the reference's x86-64 build converts it.
@@ -120,6 +148,7 @@ struct sfrt_voxel {
   // last staging reuses that slot (no host recomputation, no copy).
   uint64_t tables_version = 1, staged_version = 0;
   size_t staged_off[3] = {0, 0, 0};  // byte offsets of row | dyn | lights in the staged slot
+  float staged_xmax = 0.0f;          // max finite |component| of the staged ray directions
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
@@ -171,6 +200,7 @@ struct sfrt_voxel {
       return SFRT_OK;
     }
     std::vector<float> col((size_t)width * 3), row((size_t)height * 2);
+    float xmax = 0.0f;
     for (int i = 0; i < width; i++) {
       const float hray = (hStart + hIncreaseBy * i);
       const float fix = std::cos(cam.rotation - hray);
@@ -178,11 +208,14 @@ struct sfrt_voxel {
       col[3 * (size_t)i] = dx;
       col[3 * (size_t)i + 1] = dz;
       col[3 * (size_t)i + 2] = sfrt_math::atan2f(dz, dx);  // VAngleXZ's ray term (World.cpp:272)
+      for (float c : {dx, dz})
+        if (std::isfinite(c)) xmax = std::max(xmax, std::fabs(c));
     }
     for (int j = 0; j < height; j++) {
       const float vray = (vStart - j * vIncreaseBy);
       row[2 * (size_t)j] = (vOff + std::sin(vray));
       row[2 * (size_t)j + 1] = std::cos(cam.hrotation + vray);   // r->yscale
+      if (std::isfinite(row[2 * (size_t)j])) xmax = std::max(xmax, std::fabs(row[2 * (size_t)j]));
     }
     std::vector<sfrt::VoxDyn> vd(dyn.size());
     for (size_t k = 0; k < dyn.size(); k++) {
@@ -203,7 +236,7 @@ struct sfrt_voxel {
     for (size_t k = 0; k < lights.size(); k++) {
       const sfrt_light& L = lights[k];
       vl[k] = {L.pos[0], L.pos[1], L.pos[2], L.intensity, L.r, L.g, L.b, L.shadows,
-               light_dd_pass(L.intensity)};
+               light_dd_skip(light_dd_pass(L.intensity))};
     }
     // one blob per launch: col | row | dyn | lights, 16-byte aligned parts
     auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };
@@ -234,6 +267,7 @@ struct sfrt_voxel {
     cur_slot = next_slot;
     next_slot = (next_slot + 1) % kSlots;
     staged_version = tables_version;
+    staged_xmax = xmax;
     staged_off[0] = b_col;
     staged_off[1] = b_col + b_row;
     staged_off[2] = b_col + b_row + b_dyn;
@@ -268,6 +302,7 @@ struct sfrt_voxel {
     f.blocks = d_blocks;
     f.nx = nx; f.ny = ny; f.nz = nz;
     f.grid_bytes = (uint32_t)std::min<uint64_t>((uint64_t)nx * ny * nz * 2u, 0xffffffffu);
+    f.dda_qlim = dda_qlim(f.cam, f.maxiter, staged_xmax);
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
       f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};
       f.dyn_tex[k] = {dyn_tex[k].d, dyn_tex[k].w, dyn_tex[k].h};

@@ -42,9 +42,12 @@ struct VoxLight {                           // struct Light (World.h:40-47)
   float intensity, r, g, b;
   int32_t shadows;
   // Squared distances dd >= dd_pass have intensity / dd - dd * 0.002f <= 0 in binary32
-  // (World.cpp:425-426: the light adds nothing there): the smallest such float, found on the host
-  // by bisection over the bit patterns (the test is monotone in dd); 0 when no dd passes.
-  float dd_pass;
+  // (World.cpp:425-426: the light adds nothing there): dd_pass is the smallest such float, found
+  // on the host by bisection over the bit patterns (the test is monotone in dd; 0 when no dd
+  // passes).  The kernel's per-wave skip tests the fma-evaluated squared distance, within
+  // 6 ulp (relative 2^-20) of the reference's, against dd_skip = RU(dd_pass / (1 - 2^-20)):
+  // ddf >= dd_skip implies dd >= dd_pass.
+  float dd_skip;
 };
 
 struct VoxTex {
@@ -63,6 +66,10 @@ struct VoxFrame {
   const int16_t* blocks;                    // dense [nx][ny][nz], textureID or kVoxEmpty
   int32_t nx, ny, nz;
   uint32_t grid_bytes;                      // nx * ny * nz * 2, at most 2^32 - 1 (buffer range)
+  // The fast primary DDA's bound (sfrt_voxel.cpp dda_qlim): a ray whose direction
+  // has max|d_k| <= dda_qlim * min|d_k| keeps every DDA position below 2^30 in magnitude, where
+  // a plain v_cvt_i32_f32 equals to_i32; 0 sends every wave to the guarded DDA
+  float dda_qlim;
   VoxTex tex[kVoxSlots];
   VoxTex dyn_tex[kVoxSlots];
   uint32_t colors[kVoxSlots];               // RGBA8 packed

@@ -24,6 +24,13 @@ constexpr float kPI2 = 6.28318530718f;   // World.h:6
 __device__ __forceinline__ int32_t to_i32(float f) {
   return (f > -2147483648.0f && f < 2147483648.0f) ? (int32_t)f : (int32_t)0x80000000;
 }
+// A primary-ray DDA position to its cell coordinate: to_i32, or in the fast DDA (every lane of
+// the wave within the host's dda_qlim bound, so |f| < 2^30) the plain conversion it equals
+// there -- one v_cvt_i32_f32 instead of a compare, a conversion and a select per axis and step.
+template <bool FAST>
+__device__ __forceinline__ int32_t pos_i32(float f) {
+  return FAST ? (int32_t)f : to_i32(f);
+}
 // float -> unsigned as x86-64 g++ emits it: 64-bit cvttss2si, low 32 bits.
 __device__ __forceinline__ uint32_t to_u32(float f) {
   if (!(f > -9.2233720368547758e18f && f < 9.2233720368547758e18f)) return 0u;
@@ -79,6 +86,12 @@ __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, ui
 // outside that range (an axis-parallel ray has |dir.x| == 0) divides plainly.
 __device__ __forceinline__ bool recip_ok(float b) { return b >= 0x1.0p-60f && b <= 0x1.0p60f; }
 
+// dirXadd + sign * (pos - (float)ipos) (World.cpp:330-332, 466-468): sign is +-1, so the product
+// is exact and one fma rounds the sum exactly as the reference's add does (NaN and inf alike).
+__device__ __forceinline__ float dda_num(float add, float sign, float p, int32_t ip) {
+  return __builtin_fmaf(sign, p - (float)ip, add);
+}
+
 template <bool RECIP>
 __device__ __forceinline__ float dv(float a, float b, float y) {
   return RECIP ? sfrt_math::div_recip(a, b, y) : a / b;
@@ -120,9 +133,9 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
     work++;
     int16_t id;
     if (cell_hit(f, pix, piy, piz, id)) return false;
-    const float a = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
-    const float b = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
-    const float c = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
+    const float a = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
+    const float b = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
+    const float c = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
     float raySpeed = a;  // std::min({a, b, c})
     if (b < raySpeed) raySpeed = b;
     if (c < raySpeed) raySpeed = c;
@@ -178,10 +191,13 @@ __device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t
   for (int j = 0; j < f.nlights; j++) {
     const VoxLight L = light_at(f.lights, j);
     const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
-    float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
     // dd >= dd_pass: the light adds nothing (host threshold, exact); a wave none of whose lanes
-    // is that close skips the light's division and the rest
-    if (!__builtin_amdgcn_ballot_w64(dd < L.dd_pass)) continue;
+    // is that close skips the light's division and the rest.  The test is ours: the squared
+    // distance by two fmas against the host's inflated dd_skip (voxel_trace.h), and the body
+    // evaluates the reference's dd
+    const float ddf = __builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez));
+    if (!__builtin_amdgcn_ballot_w64(ddf < L.dd_skip)) continue;
+    float dd = ex * ex + ey * ey + ez * ez;  // VLengthS
     float add = (L.intensity / dd - dd * 0.002f);
     if (add > 0) {
       float nx = L.px - pos.x, ny = L.py - pos.y, nz = L.pz - pos.z;
@@ -213,7 +229,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   const V3 cam{f.cam[0], f.cam[1], f.cam[2]};
   float dist = 0.0f;
   V3 pos = cam;
-  int32_t pix = to_i32(pos.x), piy = to_i32(pos.y), piz = to_i32(pos.z);
+  int32_t pix = pos_i32<RECIP>(pos.x), piy = pos_i32<RECIP>(pos.y), piz = pos_i32<RECIP>(pos.z);
   // The reference's tryPos (World.cpp:318) equals pos at the top of every step (pos = tryPos
   // ends each step), so the step advances pos in place after the billboard loop, which works
   // on copies of pos and dist (the reference moves both there and then overwrites them with
@@ -238,14 +254,25 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   uint32_t early = 0u;
   for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
     work++;
-    const float xray = dv<RECIP>(dirxadd + sx * (pos.x - (float)pix), lx, yx);
-    const float yray = dv<RECIP>(diryadd + sy * (pos.y - (float)piy), ly, yy);
-    const float zray = dv<RECIP>(dirzadd + sz * (pos.z - (float)piz), lz, yz);
+    const float xray = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
+    const float yray = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
+    const float zray = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
     // the reference's if / else-if / else (World.cpp:330-350) as selects: one branch-free step
-    // (as branches the compiler built an exec-mask diamond with ~12 scalar instructions)
-    const bool ax = (xray <= yray) & (xray <= zray);
-    const bool ay = !ax & (yray <= xray) & (yray <= zray);
-    const float raySpeed = ax ? xray : (ay ? yray : zray);
+    // (as branches the compiler built an exec-mask diamond with ~12 scalar instructions).  In the
+    // fast DDA no ray is NaN (finite numerators over |d| >= 2^-60) and a zero ray is +0 (the
+    // numerator is +0 or nonzero), so the chosen ray is the minimum (v_min3_f32) and the
+    // reference's first axis holding it
+    bool ax, ay;
+    float raySpeed;
+    if (RECIP) {
+      raySpeed = fminf(fminf(xray, yray), zray);
+      ax = xray == raySpeed;
+      ay = !ax & (yray == raySpeed);
+    } else {
+      ax = (xray <= yray) & (xray <= zray);
+      ay = !ax & (yray <= xray) & (yray <= zray);
+      raySpeed = ax ? xray : (ay ? yray : zray);
+    }
     const float rs2 = raySpeed + 0.002f;
     colRay = ax ? 1 : (ay ? 2 : 3);
     const float tryDist = dist + raySpeed;
@@ -295,7 +322,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     pos.x += dir.x * (ax ? rs2 : raySpeed);  // tryPos (World.cpp:330-350)
     pos.y += dir.y * (ay ? rs2 : raySpeed);
     pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
-    pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
+    pix = pos_i32<RECIP>(pos.x); piy = pos_i32<RECIP>(pos.y); piz = pos_i32<RECIP>(pos.z);
     int16_t id;
     if (cell_hit(f, pix, piy, piz, id)) {  // hit a block (World.cpp:385)
       hit = true;
@@ -311,7 +338,11 @@ done:
 
 __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
                             float atan_dir, uint32_t& work) {
-  const bool ok = recip_ok(fabsf(dir.x)) && recip_ok(fabsf(dir.y)) && recip_ok(fabsf(dir.z));
+  // the reciprocal divisions and, within the host's bound on the direction's spread, the plain
+  // position conversions (pos_i32)
+  const float lx = fabsf(dir.x), ly = fabsf(dir.y), lz = fabsf(dir.z);
+  const bool ok = recip_ok(lx) && recip_ok(ly) && recip_ok(lz) &&
+                  fmaxf(fmaxf(lx, ly), lz) <= f.dda_qlim * fminf(fminf(lx, ly), lz);
   if (__builtin_amdgcn_ballot_w64(!ok)) return raycast_t<false>(f, dir, yscale, atan_dir, work);
   return raycast_t<true>(f, dir, yscale, atan_dir, work);
 }

@@ -224,6 +224,12 @@ VOXEL_EDGE_CASES = [  # (width, height, cam_pos, rotation, hrotation, what)
     (320, 180, (16.0, 2.0, 16.0), 1.0, 0.2, "integer_position"),
     # looking straight along the floor far away: long DDA walks up to maxiter
     (320, 180, (1.5, 0.5, 1.5), 0.785398, 0.0, "long_walks"),
+    # the fast primary DDA's host bound (sfrt_voxel.cpp dda_qlim) off: a camera beyond 2^30
+    # sends every wave to the guarded conversions, and one just below 2^31 walks past it, where
+    # the reference's cvttss2si gives INT_MIN (to_i32) and a plain conversion would saturate
+    (320, 180, (1.5e9, 1.9, 15.5), 3.14159, 0.0, "far_camera"),
+    (320, 180, (2147483520.0, 1.9, 15.5), 0.0, 0.0, "camera_at_int_limit"),
+    (320, 180, (2147483520.0, 1.9, 15.5), 3.14159, 0.0, "camera_at_int_limit_back"),
 ]
 
 
@@ -259,8 +265,10 @@ def test_voxel_gpu_edge_poses_match_oracle(vworld, assets, case):
     bad = np.nonzero(np.any(g != wv, axis=1))[0]
     assert bad.size == 0, (f"{bad.size} pixels differ, first ({bad[0] % w}, {bad[0] // w}): "
                            f"gpu={g[bad[0]]} oracle={wv[bad[0]]}")
-    # the frame is not trivially empty: some pixel is not the background
-    assert len(np.unique(g, axis=0)) > 4
+    # the frame is not trivially empty: some pixel is not the background (far from the grid
+    # every ray runs out of steps in empty space)
+    if not case[-1].startswith(("far_", "camera_at_")):
+        assert len(np.unique(g, axis=0)) > 4
 
 
 def test_light_dd_pass_is_the_exact_threshold(built):
@@ -287,3 +295,56 @@ def test_light_dd_pass_is_the_exact_threshold(built):
         assert adds(i, np.nextafter(t, f32(0))), (i, t)
         for m in (1.0001, 1.5, 10.0, 1e6):
             assert not adds(i, f32(t * f32(m))), (i, t, m)
+
+
+def test_fast_dda_step_bound():
+    """The fast primary DDA's bound (sfrt_voxel.cpp dda_qlim): one step of World::Raycast
+    (World.cpp:330-350, binary32 as numpy evaluates it) moves each coordinate by at most
+    2.001 Q + 0.003 X + 33 with X = max|d_k|, Q = X / min|d_k|, for positions below 2^30 --
+    including negative positions, whose negative fractions give negative ray speeds, and
+    directions with tiny components.  CPU only: random walks from cameras spread over
+    [-2^29, 2^29] with directions spread over twenty binades."""
+    f32 = np.float32
+    rng = np.random.default_rng(7)
+    n = 20000
+    d = (rng.choice([-1.0, 1.0], (n, 3)) * 2.0 ** rng.uniform(-12, 8, (n, 3))).astype(f32)
+    p = (rng.choice([-1.0, 1.0], (n, 3)) * 2.0 ** rng.uniform(-4, 29, (n, 3))).astype(f32)
+    ad = np.abs(d)
+    X = ad.max(axis=1).astype(np.float64)
+    Q = X / ad.min(axis=1)
+    S = 2.001 * Q + 0.003 * X + 33.0
+    add = (d > 0).astype(f32)
+    sgn = np.where(d > 0, f32(-1), f32(1))
+    with np.errstate(over="ignore", invalid="ignore"):
+        for _ in range(40):
+            ip = np.trunc(p)                               # (float)(int)pos, |pos| < 2^30
+            ray = (add + sgn * (p - ip)).astype(f32) / ad  # xray, yray, zray
+            ax = (ray[:, 0] <= ray[:, 1]) & (ray[:, 0] <= ray[:, 2])
+            ay = ~ax & (ray[:, 1] <= ray[:, 0]) & (ray[:, 1] <= ray[:, 2])
+            rs = np.where(ax, ray[:, 0], np.where(ay, ray[:, 1], ray[:, 2])).astype(f32)
+            rs2 = (rs + f32(0.002)).astype(f32)
+            step = np.stack([np.where(ax, rs2, rs), np.where(ay, rs2, rs),
+                             np.where(ax | ay, rs, rs2)], axis=1).astype(f32)
+            q = (p + (d * step).astype(f32)).astype(f32)
+            live = np.all(np.abs(q) < 2.0 ** 30, axis=1) & np.all(np.abs(p) < 2.0 ** 30, axis=1)
+            moved = np.abs(q.astype(np.float64) - p.astype(np.float64)).max(axis=1)
+            assert np.all(moved[live] <= S[live]), moved[live][moved[live] > S[live]][:5]
+            p = np.where(live[:, None], q, p)
+
+
+def test_light_skip_fma_distance_bound():
+    """The kernel's per-wave light skip tests ddf = fma(ex, ex, fma(ey, ey, ez * ez)) against
+    dd_skip = RU(dd_pass / (1 - 2^-20)) (voxel_trace.h VoxLight): sound because the reference's
+    dd = (ex*ex + ey*ey) + ez*ez (World.cpp:424, binary32) is never below ddf * (1 - 2^-20).
+    CPU only: 10^6 random offsets over sixty binades, fma emulated in binary64 (the products of
+    binary32 values are exact there)."""
+    f32 = np.float32
+    rng = np.random.default_rng(11)
+    n = 1_000_000
+    e = (rng.choice([-1.0, 1.0], (n, 3)) * 2.0 ** rng.uniform(-30, 30, (n, 3))).astype(f32)
+    ex, ey, ez = (e[:, k] for k in range(3))
+    dd = ((ex * ex + ey * ey).astype(f32) + ez * ez).astype(f32)
+    zz = (ez * ez).astype(f32)
+    inner = (ey.astype(np.float64) * ey + zz).astype(f32)
+    ddf = (ex.astype(np.float64) * ex + inner).astype(f32)
+    assert np.all(dd.astype(np.float64) >= ddf.astype(np.float64) * (1.0 - 2.0 ** -20))

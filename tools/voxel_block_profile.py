@@ -52,7 +52,7 @@ ANCHORS = {  # one line each in voxel_trace.hip
     "billboard_last": "dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf(\"\");\n      }",
     "light_loop": "for (int j = 0; j < f.nlights; j++) {",
     "shadow_loop": "for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {",
-    "light_skip": "if (!__builtin_amdgcn_ballot_w64(dd < L.dd_pass)) continue;",
+    "light_skip": "if (!__builtin_amdgcn_ballot_w64(ddf < L.dd_skip)) continue;",
 }
 
 
@@ -247,8 +247,8 @@ def build():
         ("  uint32_t c;\n  if (id < 0) {", "  cnt[2] += first_lane_here();\n  uint32_t c;\n  if (id < 0) {"),
         ("    const VoxLight L = light_at(f.lights, j);\n",
          "    const VoxLight L = light_at(f.lights, j);\n    cnt[3] += first_lane_here();\n"),
-        ("    if (!__builtin_amdgcn_ballot_w64(dd < L.dd_pass)) continue;\n",
-         "    if (!__builtin_amdgcn_ballot_w64(dd < L.dd_pass)) continue;\n"
+        ("    if (!__builtin_amdgcn_ballot_w64(ddf < L.dd_skip)) continue;\n",
+         "    if (!__builtin_amdgcn_ballot_w64(ddf < L.dd_skip)) continue;\n"
          "    cnt[6] += first_lane_here();\n"),
         ("  uint32_t work = 0;\n  const int i = f.xstart", "  uint32_t work = 0;\n"
          "  uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};\n  const int i = f.xstart"),
