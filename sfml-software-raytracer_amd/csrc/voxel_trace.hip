@@ -259,9 +259,12 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
     const float zray = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
     // the reference's if / else-if / else (World.cpp:330-350) as selects: one branch-free step
     // (as branches the compiler built an exec-mask diamond with ~12 scalar instructions).  In the
-    // fast DDA no ray is NaN (finite numerators over |d| >= 2^-60) and a zero ray is +0 (the
-    // numerator is +0 or nonzero), so the chosen ray is the minimum (v_min3_f32) and the
-    // reference's first axis holding it
+    // fast DDA no ray is NaN (finite numerators over |d| >= 2^-60), so the reference's choice is
+    // the first axis whose ray equals the minimum (v_min3_f32; +-0 compare equal).  The speed
+    // can differ from the reference's only in the sign of a zero (a negative ray underflowing to
+    // -0 beside a +0 one), which reaches the position only through dir * speed added to a -0.0
+    // component (a -0.0 camera coordinate not yet moved), and no output depends on that sign
+    // (to_i32, the fractions, the texel and light offsets all map +-0 alike)
     bool ax, ay;
     float raySpeed;
     if (RECIP) {
