@@ -166,24 +166,19 @@ __device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t
   if (id < 0) {
     c = f.colors[-id];
   } else {
+    // the reference's three face branches (World.cpp:395-412) as selects of the same
+    // expressions: one texel fetch per lane whatever mix of faces the wave's lanes hit
     const VoxTex& t = f.tex[id];
     const float tw = (float)(uint32_t)t.w, th = (float)(uint32_t)t.h;
-    if (colRay == 1) {
-      c = texel(f, t, to_u32(tw * (pos.z - (float)piz)), to_u32(th * (pos.y - (float)piy)));
-      pos.x += sx * 0.01f;  // get it off the wall
-      sy = 0.0f;
-      sz = 0.0f;
-    } else if (colRay == 2) {
-      c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.z - (float)piz)));
-      pos.y += sy * 0.01f;
-      sx = 0.0f;
-      sz = 0.0f;
-    } else {
-      c = texel(f, t, to_u32(tw * (pos.x - (float)pix)), to_u32(th * (pos.y - (float)piy)));
-      pos.z += sz * 0.01f;
-      sx = 0.0f;
-      sy = 0.0f;
-    }
+    const float fx = pos.x - (float)pix, fy = pos.y - (float)piy, fz = pos.z - (float)piz;
+    const bool c1 = colRay == 1, c2 = colRay == 2, c3 = !c1 & !c2;
+    c = texel(f, t, to_u32(tw * (c1 ? fz : fx)), to_u32(th * (c2 ? fz : fy)));
+    pos.x = c1 ? pos.x + sx * 0.01f : pos.x;  // get it off the wall
+    pos.y = c2 ? pos.y + sy * 0.01f : pos.y;
+    pos.z = c3 ? pos.z + sz * 0.01f : pos.z;
+    sx = c1 ? sx : 0.0f;
+    sy = c2 ? sy : 0.0f;
+    sz = c3 ? sz : 0.0f;
   }
   const float l0 = 0.05f / dist - dist * 0.0001f;
   float litr = l0 < 0.0f ? 0.0f : l0;
