@@ -561,7 +561,144 @@ def valu_fraction(pixels: int, kernel: str, kernel_ms: float):
     return out
 
 
-def main() -> None:
+SUPERVISOR_TIME_LIMIT_S = 1500
+PG_TIMEOUT_S = 300
+
+
+def _partial_write(path, result) -> None:
+    """Rank 0's line so far (bench.py --partial-out): the supervisor prints it, with the
+    failure under "error", if this process dies or hangs before printing the full line."""
+    if not path or result is None:
+        return
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(result, f)
+    os.replace(tmp, path)
+
+
+def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
+    """N > 1 (one process per GPU under torch.distributed.run): this rank's body runs in a child
+    process (bench.py --worker), so that an RCCL failure -- communicator init, a collective on
+    device bands, a hang in the tuner -- ends in ONE parseable JSON line from rank 0 with an
+    "error" field instead of a crash or a hang without output.  The supervisor never touches the
+    GPU (the child is the only process that initialises HIP).  It relays the child's output; the
+    child runs under a process-group timeout (PG_TIMEOUT_S, so a stuck collective raises) and the
+    supervisor's own limit.  If the child fails, hangs past `time_limit` or the supervisor is
+    signalled (torch.distributed.run ends every rank when one rank fails), rank 0 prints the line
+    the child had reached (--partial-out: the headline once measured, then every also line) with
+    "error" = {stage, exit, detail}, or a line with "value": null when the headline was not
+    reached.  Exit status: 0 when the printed line carries a measured headline, else 1; ranks != 0
+    pass their child's status on.  Reference caller: Source.cpp:47-52."""
+    import collections
+    import signal
+    import subprocess
+    import tempfile
+    import threading
+    partial = None
+    if rank == 0:
+        fd, partial = tempfile.mkstemp(prefix="bench_partial_", suffix=".json")
+        os.close(fd)
+        os.unlink(partial)
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + list(argv) + ["--worker"]
+    if partial:
+        cmd += ["--partial-out", partial]
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+    seen = {"line": False}
+    tail = collections.deque(maxlen=12)
+
+    def relay(src, dst, keep):
+        for ln in src:
+            if keep:
+                tail.append(ln.rstrip())
+            elif ln.startswith('{"metric"'):
+                seen["line"] = True
+            dst.write(ln)
+            dst.flush()
+    threads = [threading.Thread(target=relay, args=(child.stdout, sys.stdout, False), daemon=True),
+               threading.Thread(target=relay, args=(child.stderr, sys.stderr, True), daemon=True)]
+    for t in threads:
+        t.start()
+    why = {"signal": None}
+
+    def stop_child():
+        for sig, wait in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(child.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                child.wait(timeout=wait)
+                return
+            except subprocess.TimeoutExpired:
+                continue
+
+    def on_signal(signum, _frame):
+        why["signal"] = signal.Signals(signum).name
+        stop_child()
+    for sg in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sg, on_signal)
+    deadline = time.monotonic() + time_limit
+    timed_out = False
+    while child.poll() is None:
+        if time.monotonic() > deadline:
+            timed_out = True
+            stop_child()
+            break
+        time.sleep(0.2)
+    rc = child.wait()
+    for t in threads:
+        t.join(timeout=5)
+    if rank != 0:
+        return rc if rc >= 0 else 1
+    line = None
+    if partial and os.path.exists(partial):
+        try:
+            line = json.load(open(partial))
+        except (OSError, ValueError):
+            line = None
+        os.unlink(partial)
+    if rc == 0 and seen["line"] and not (timed_out or why["signal"]):
+        return 0
+    if seen["line"]:  # the full line is out (rc 3: it reports frames that differ)
+        if rc != 3:
+            print(f"bench supervisor: rank 0 exited {rc} after printing its line", file=sys.stderr)
+        return 3 if rc == 3 else 0
+    if timed_out:
+        cause = f"time limit {time_limit:.0f} s (supervisor)"
+    elif why["signal"]:
+        cause = f"supervisor received {why['signal']} (another rank failed?)"
+    else:
+        cause = f"rank 0 body exited {rc}"
+    headline = line is not None and line.get("value") is not None
+    if line is None:
+        line = {"metric": "Mrays/s (primary rays, full RGBA8 frames in HBM)", "value": None,
+                "unit": "Mrays/s", "n_gpus": world_size, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic"}
+    line["error"] = {"stage": line.pop("_stage", "before the headline"), "cause": cause,
+                     "exit": rc, "detail": list(tail)[-6:]}
+    line["complete"] = False
+    print(json.dumps(line), flush=True)
+    return 0 if headline else 1
+
+
+def injected_failure(args, rank: int, world_size: int, where: str) -> None:
+    """TEST ONLY (--inject-failure MODE@WHERE, tests/test_bench_failures.py): rank 1 fails at
+    `where` while the other ranks enter a collective: "raise" raises, "exit" ends the process
+    abruptly, "hang" blocks until killed.  Never part of a measurement."""
+    mode = args.inject_failure.split("@")[0]
+    if rank == 1:
+        print(f"rank 1: injected failure {args.inject_failure}", file=sys.stderr, flush=True)
+        if mode == "raise":
+            raise RuntimeError(f"injected failure at {where}")
+        if mode == "exit":
+            os._exit(7)
+        while True:
+            time.sleep(1)
+    dist.barrier()  # never completes: rank 1 does not join
+
+
+def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -591,20 +728,38 @@ def main() -> None:
     ap.add_argument("--headline-only", action="store_true",
                     help="only the headline workload (no also lines, no CPU baseline): the command "
                          "whose rocprof kernel trace profiles/*_kernel_stats_by_grid.csv summarises")
+    ap.add_argument("--time-limit", type=float, default=SUPERVISOR_TIME_LIMIT_S,
+                    help="N > 1: seconds before the supervisor ends a rank's body and rank 0 "
+                         "prints the line reached so far with an error field")
+    ap.add_argument("--pg-timeout", type=float, default=PG_TIMEOUT_S,
+                    help="N > 1: process-group timeout in seconds (a collective stuck longer raises)")
+    ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--partial-out", type=str, default="", help=argparse.SUPPRESS)
+    ap.add_argument("--inject-failure", type=str, default="",
+                    help="TEST ONLY (MODE@WHERE, MODE raise|exit|hang, WHERE init|also): rank 1 "
+                         "fails there; the run then ends in rank 0's error line")
     args = ap.parse_args()
     also_steps, also_warmup = max(20, args.also_steps), max(5, args.also_warmup)
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size > 1 and not (args.worker or args.c_abi_child):
+        return supervise(sys.argv[1:], rank, world_size, args.time_limit)
+    from datetime import timedelta
+    pg_timeout = timedelta(seconds=args.pg_timeout)
+    if args.inject_failure.endswith("@init"):  # TEST ONLY: no GPU needed
+        dist.init_process_group("gloo", timeout=pg_timeout)
+        injected_failure(args, rank, world_size, "init")
+        return 1
 
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU fallback)")
     if args.c_abi_child:
         c_abi_child(args.c_abi_child, args.also_steps, args.also_warmup, args.also_settle)
-        return
+        return 0
     if sfrt.build_flavour() != "release":
         raise SystemExit(f"bench.py measures the release library only; {sfrt.LIB_PATH} reports "
                          f"build flavour {sfrt.build_flavour()!r} (unset SFRT_LIB, rebuild)")
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
     device = 0 if args.rehearse else local_rank
@@ -612,13 +767,15 @@ def main() -> None:
     host_group = None
     if world_size > 1:
         if args.rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
             bands_mod.stage_p2p_through_host()
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank),
+                                    timeout=pg_timeout)
         # a host-side barrier for the c_abi_multi line: ranks waiting on an RCCL barrier
         # would keep a kernel spinning on the GPUs rank 0 renders on
-        host_group = dist.new_group(backend="gloo")
+        host_group = dist.new_group(backend="gloo",
+                                    timeout=timedelta(seconds=C_ABI_CHILD_TIMEOUT_S + 120))
 
     floor = scenes.load_floor()
     scene = scenes.lcg64()
@@ -711,6 +868,10 @@ def main() -> None:
         w.check(stream.cuda_stream)
         result["gathered_frame_bit_identical"] = bool(torch.equal(single, frame))
         del single
+    if rank == 0:
+        _partial_write(args.partial_out, dict(result, _stage="after the headline"))
+    if args.inject_failure.endswith("@also"):  # TEST ONLY
+        injected_failure(args, rank, world_size, "also")
     # Larger frames of the BASELINE configs (strong scaling: the frame is fixed,
     # its rows split over the ranks), measured after the main line.
     extra = {}
@@ -723,6 +884,9 @@ def main() -> None:
                 line["hbm_frac"] = line.pop("hbm_frac_rank0_kernel")
                 line["kernel_ms"] = line.pop("kernel_ms_rank0_band")
             extra[f"{fw}x{fh}_{sname}"] = line
+            if rank == 0:
+                _partial_write(args.partial_out, dict(result, also=dict(extra),
+                                                      _stage=f"after also/{fw}x{fh}_{sname}"))
         w.set_scene(scene, WIDTH, height)
     if rank == 0:
         result["also"] = dict(extra)
@@ -849,13 +1013,38 @@ def main() -> None:
             note="PCIe-inclusive (frame copied into a host buffer), not the HBM-resident value")
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(scene, WIDTH, height, floor, gpu_frame)
+    rc = 0
     if rank == 0:
+        # every frame the line checked must be bit-identical to its golden / one-GPU frame; a line
+        # with any that differs is marked invalid and the run exits 3 (after printing it)
+        bad = [k for k, v in bit_identity_flags(result) if v is not True]
+        result["all_frames_bit_identical"] = not bad
+        if bad:
+            result["invalid"] = {"frames_differ": bad}
+            rc = 3
         print(json.dumps(result), flush=True)
     w.close()
     if world_size > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return rc
+
+
+def bit_identity_flags(obj, path=""):
+    """(path, value) of every bit-identity flag in a result line (keys naming bit_identical)."""
+    out = []
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            p = f"{path}/{k}" if path else k
+            if "bit_identical" in k and not isinstance(v, (dict, list)):
+                out.append((p, v))
+            else:
+                out += bit_identity_flags(v, p)
+    elif isinstance(obj, list):
+        for i, v in enumerate(obj):
+            out += bit_identity_flags(v, f"{path}[{i}]")
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

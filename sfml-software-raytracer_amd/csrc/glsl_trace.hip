@@ -102,6 +102,38 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   // (host-checked with the same test), so they change nothing; a whole pass
   // in which no lane of the wave is inside a wall leaves the state at a fixed
   // point, so the remaining passes would repeat it and are skipped.
+#if SFRT_GLSL_LOOPS
+  // The passes as an outer loop and the walls as a counted inner loop (the record address
+  // stepped, not recomputed): the single loop with its wrap-around index kept ~20 scalar
+  // instructions per wall visit (tools/isa_block_profile.py).
+  if (f.sc > 0) {
+    int k = f.wall_start % f.sc;
+    for (int pass = f.wall_start / f.sc; pass < 3; pass++) {
+      uint64_t moved = 0;
+      for (; k < f.sc; k++) {
+        const GlslWall w = ld(walls, k);
+        const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
+        const float s = (rx * rx + ry * ry) + rz * rz;
+        const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
+        const uint64_t inside_mask = __builtin_amdgcn_ballot_w64(inside);  // scalar tests only
+        if ((inside_mask | (uint64_t)(uint32_t)f.cam_negzero) != 0) {
+          moved |= inside_mask;
+          const float cs = inside ? 1.0f : 0.0f;
+          const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
+          const float c = cs * s - w.rr;
+          const float tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
+          px = px + dx * tosurf;
+          py = py + dy * tosurf;
+          pz = pz + dz * tosurf;
+          total = total + tosurf;
+        }
+        draw = inside ? k : draw;
+      }
+      k = 0;
+      if (!moved) break;  // uniform: a pass in which no lane moved is a fixed point
+    }
+  }
+#else
   bool moved = false;
   for (int j = f.wall_start, k = f.wall_start % (f.sc > 0 ? f.sc : 1); j < 3 * f.sc; j++) {
     const GlslWall w = ld(walls, k);
@@ -133,6 +165,8 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
     }
   }
 
+#endif
+
   // ---- metaball march over lights + ospheres (:87-112) ----
   const int nballs = f.all - f.sc;
   float ball_dist = 0.0f;
@@ -140,11 +174,19 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   int closest = 0;
   float snx = 0.0f, sny = 0.0f, snz = 0.0f;
   int steps = 0;
+#if SFRT_GLSL_LOOPS
+  // One way out of the march: the shader's loop test and our step cap as one condition at the
+  // bottom (the cap's status after the loop): two divergent exits cost a lane mask merge each.
+  if (ball_dist < total && smooth > 0.01f) {
+  for (;;) {
+    ++steps;
+#else
   while (ball_dist < total && smooth > 0.01f) {
     if (++steps > kGlslMarchCap) {
       atomicOr(f.status, 1);
       break;
     }
+#endif
     const float tx = cx + dx * ball_dist, ty = cy + dy * ball_dist, tz = cz + dz * ball_dist;
     smooth = 999999999.0f;
     closest = 0;
@@ -180,7 +222,14 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
       thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
     }
     ball_dist += smooth + 0.01f;
+#if SFRT_GLSL_LOOPS
+    if (!((ball_dist < total) & (smooth > 0.01f) & (steps < kGlslMarchCap))) break;
   }
+  if (steps == kGlslMarchCap && ball_dist < total && smooth > 0.01f) atomicOr(f.status, 1);
+  }
+#else
+  }
+#endif
   work = (uint32_t)steps;
 
   // ---- wall or ball (:114-120) ----

@@ -105,15 +105,9 @@ struct sfrt_glsl {
   // Per-draw tables (walls | balls | pairs | mats) in a ring of slots, each
   // with a pinned staging copy and the event of the last draw that read it,
   // so draws on different streams never overwrite tables still in use.
-  struct TableSlot {
-    void* d = nullptr;
-    void* h = nullptr;
-    size_t cap = 0;
-    hipEvent_t ev = nullptr;
-    bool pending = false;
-  };
+  // (sfrt::TableSlot, sfrt_host.h: a reuse on another stream waits for the slot's last user.)
   static constexpr int kSlots = 4;
-  TableSlot slots[kSlots];
+  sfrt::TableSlot slots[kSlots];
   int next_slot = 0;
   int cur_slot = -1;
   // The tables depend only on the uniform block: every uniform setter bumps u_version, and a
@@ -132,11 +126,7 @@ struct sfrt_glsl {
     (void)hipDeviceSynchronize();
     sched.release();
     (void)hipFree(d_mip);
-    for (auto& t : slots) {
-      (void)hipFree(t.d);
-      (void)hipHostFree(t.h);
-      if (t.ev) (void)hipEventDestroy(t.ev);
-    }
+    for (auto& t : slots) t.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
     if (stream) (void)hipStreamDestroy(stream);
@@ -219,6 +209,7 @@ struct sfrt_glsl {
       f.wall_start = j < sc ? j : 3 * sc;  // inside no wall: no lane ever moves
     }
     if (staged_version == u_version && cur_slot >= 0) {  // launched() re-marks the slot
+      HIP_TRY(slots[cur_slot].use_on(s));  // staged, or last read, on another stream: wait for it
       fill_tables(f, (uint8_t*)slots[cur_slot].d, staged_off);
       return SFRT_OK;
     }
@@ -266,10 +257,8 @@ struct sfrt_glsl {
     const size_t bw = walls.size() * sizeof walls[0], bb = balls.size() * sizeof balls[0],
                  bp = pairs.size() * sizeof pairs[0], bm = mats.size() * sizeof mats[0];
     const size_t bytes = bw + bb + bp + bm;
-    TableSlot& t = slots[next_slot];
-    if (t.pending) HIP_TRY(hipEventSynchronize(t.ev));
-    t.pending = false;
-    if (!t.ev) HIP_TRY(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
+    sfrt::TableSlot& t = slots[next_slot];
+    HIP_TRY(t.reclaim());
     if (t.cap < bytes) {
       (void)hipFree(t.d);
       (void)hipHostFree(t.h);
@@ -285,6 +274,7 @@ struct sfrt_glsl {
     std::memcpy(blob + bw + bb, pairs.data(), bp);
     std::memcpy(blob + bw + bb + bp, mats.data(), bm);
     HIP_TRY(hipMemcpyAsync(t.d, blob, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(t.staged(s));
     cur_slot = next_slot;
     next_slot = (next_slot + 1) % kSlots;
     staged_version = u_version;
@@ -313,9 +303,7 @@ struct sfrt_glsl {
 
   // Marks the current table slot busy until the work queued on s completes.
   int launched(hipStream_t s) {
-    TableSlot& t = slots[cur_slot];
-    HIP_TRY(hipEventRecord(t.ev, s));
-    t.pending = true;
+    HIP_TRY(slots[cur_slot].launched(s));
     return SFRT_OK;
   }
 

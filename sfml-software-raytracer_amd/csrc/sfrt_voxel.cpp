@@ -126,21 +126,15 @@ struct sfrt_voxel {
   // --- device resources ---
   hipStream_t stream = nullptr;
   DevTex tex[sfrt::kVoxSlots], dyn_tex[sfrt::kVoxSlots];
-  int16_t* d_blocks = nullptr;
-  size_t d_blocks_cap = 0;
+  uint8_t* d_cells = nullptr;  // the key-indexed byte grid (voxel_trace.h, cell_hit)
+  size_t d_cells_cap = 0;
   bool blocks_dirty = true;
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
   // launches on different streams never see a table overwritten under them.
-  struct TableSlot {
-    void* d = nullptr;
-    void* h = nullptr;
-    size_t cap = 0;
-    hipEvent_t ev = nullptr;
-    bool pending = false;
-  };
+  // (sfrt::TableSlot, sfrt_host.h: a reuse on another stream waits for the slot's last user.)
   static constexpr int kSlots = 4;
-  TableSlot slots[kSlots];
+  sfrt::TableSlot slots[kSlots];
   int next_slot = 0;
   int cur_slot = -1;
   // The tables depend only on the size, the camera, the billboards and the lights: every
@@ -164,12 +158,8 @@ struct sfrt_voxel {
     for (auto& t : tex) (void)hipFree(t.d);
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
-    (void)hipFree(d_blocks);
-    for (auto& t : slots) {
-      (void)hipFree(t.d);
-      (void)hipHostFree(t.h);
-      if (t.ev) (void)hipEventDestroy(t.ev);
-    }
+    (void)hipFree(d_cells);
+    for (auto& t : slots) t.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
     if (stream) (void)hipStreamDestroy(stream);
@@ -193,9 +183,10 @@ struct sfrt_voxel {
     const float hStart = cam.rotation - cam.fov_h / 2;
     const float hIncreaseBy = cam.fov_h / width;
     if (staged_version == tables_version && cur_slot >= 0) {
-      TableSlot& t = slots[cur_slot];  // still holds this scene's tables; launched() re-marks it
-      const int rc = blocks_upload();  // first: fill_frame reads d_blocks
+      sfrt::TableSlot& t = slots[cur_slot];  // still holds this scene's tables; launched() re-marks it
+      const int rc = blocks_upload();  // first: fill_frame reads d_cells
       if (rc != SFRT_OK) return rc;
+      HIP_TRY(t.use_on(s));  // staged, or last read, on another stream: wait for it
       fill_frame(f, (uint8_t*)t.d, staged_off);
       return SFRT_OK;
     }
@@ -244,10 +235,8 @@ struct sfrt_voxel {
                  b_dyn = up16(vd.size() * sizeof(sfrt::VoxDyn)),
                  b_lit = up16(vl.size() * sizeof(sfrt::VoxLight));
     const size_t bytes = b_col + b_row + b_dyn + b_lit + 16;
-    TableSlot& t = slots[next_slot];
-    if (t.pending) HIP_TRY(hipEventSynchronize(t.ev));
-    t.pending = false;
-    if (!t.ev) HIP_TRY(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
+    sfrt::TableSlot& t = slots[next_slot];
+    HIP_TRY(t.reclaim());
     if (t.cap < bytes) {
       (void)hipFree(t.d);
       (void)hipHostFree(t.h);
@@ -264,6 +253,7 @@ struct sfrt_voxel {
     if (!vl.empty())
       std::memcpy(h + b_col + b_row + b_dyn, vl.data(), vl.size() * sizeof(sfrt::VoxLight));
     HIP_TRY(hipMemcpyAsync(t.d, t.h, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(t.staged(s));
     cur_slot = next_slot;
     next_slot = (next_slot + 1) % kSlots;
     staged_version = tables_version;
@@ -271,37 +261,45 @@ struct sfrt_voxel {
     staged_off[0] = b_col;
     staged_off[1] = b_col + b_row;
     staged_off[2] = b_col + b_row + b_dyn;
-    const int rc = blocks_upload();  // first: fill_frame reads d_blocks
+    const int rc = blocks_upload();  // first: fill_frame reads d_cells
     if (rc != SFRT_OK) return rc;
     fill_frame(f, (uint8_t*)t.d, staged_off);
     return SFRT_OK;
   }
 
+  // The world as the kernel reads it: byte (x << 20) + (y << 10) + z = id + kVoxCellBias of the
+  // block at (x, y, z), 0 elsewhere (the reference's map key as a linear index, voxel_trace.h).
+  // nx planes of 1 MiB; each plane's ny rows of nz codes land at row pitch 1024.
   int blocks_upload() {
     if (blocks_dirty) {  // rare: launches on any stream may still read the old grid
       HIP_TRY(hipDeviceSynchronize());
-      if (d_blocks_cap < blocks.size()) {
-        (void)hipFree(d_blocks);
-        d_blocks = nullptr;
-        d_blocks_cap = 0;
-        HIP_TRY(hipMalloc(&d_blocks, blocks.size() * sizeof(int16_t)));
-        d_blocks_cap = blocks.size();
+      const size_t bytes = (size_t)nx << 20;
+      if (d_cells_cap < bytes) {
+        (void)hipFree(d_cells);
+        d_cells = nullptr;
+        d_cells_cap = 0;
+        HIP_TRY(hipMalloc(&d_cells, bytes));
+        d_cells_cap = bytes;
       }
-      HIP_TRY(hipMemcpy(d_blocks, blocks.data(), blocks.size() * sizeof(int16_t),
-                        hipMemcpyHostToDevice));
+      HIP_TRY(hipMemset(d_cells, 0, bytes));
+      std::vector<uint8_t> code(blocks.size());
+      for (size_t k = 0; k < blocks.size(); k++)
+        code[k] = blocks[k] == sfrt::kVoxEmpty ? 0 : (uint8_t)(blocks[k] + sfrt::kVoxCellBias);
+      for (int x = 0; x < nx; x++)
+        HIP_TRY(hipMemcpy2D(d_cells + ((size_t)x << 20), 1024, code.data() + (size_t)x * ny * nz,
+                            (size_t)nz, (size_t)nz, (size_t)ny, hipMemcpyHostToDevice));
       blocks_dirty = false;
     }
     return SFRT_OK;
   }
 
   // The frame record's device pointers: the staged tables at d, the grid (blocks_upload()
-  // must have run: the kernel's buffer resource over d_blocks has no other guard).
+  // must have run: the kernel's buffer resource over d_cells has no other guard).
   void fill_frame(sfrt::VoxFrame& f, uint8_t* d, const size_t* off) {
     f.col = (const float*)d;
     f.row = (const float*)(d + off[0]);
-    f.blocks = d_blocks;
-    f.nx = nx; f.ny = ny; f.nz = nz;
-    f.grid_bytes = (uint32_t)std::min<uint64_t>((uint64_t)nx * ny * nz * 2u, 0xffffffffu);
+    f.cells = d_cells;
+    f.cell_bytes = (uint32_t)nx << 20;
     f.dda_qlim = dda_qlim(f.cam, f.maxiter, staged_xmax);
     for (int k = 0; k < sfrt::kVoxSlots; k++) {
       f.tex[k] = {tex[k].d, tex[k].w, tex[k].h};
@@ -317,9 +315,7 @@ struct sfrt_voxel {
 
   // Marks the current table slot busy until the work queued on s completes.
   int launched(hipStream_t s) {
-    TableSlot& t = slots[cur_slot];
-    HIP_TRY(hipEventRecord(t.ev, s));
-    t.pending = true;
+    HIP_TRY(slots[cur_slot].launched(s));
     return SFRT_OK;
   }
 

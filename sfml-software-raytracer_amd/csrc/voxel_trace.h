@@ -15,17 +15,16 @@ namespace sfrt {
 
 constexpr int kVoxSlots = 10;              // textures / dynTextures / colors (World.h:90-92)
 constexpr int16_t kVoxEmpty = -32768;
-// Dense block grid limits (sfrt_voxel_set_blocks refuses larger grids): the reference's map key
-// (x << 20) + (y << 10) + z (World.cpp:385) addresses x < 2048, y, z < 1024 without overlap, and
-// cell_hit (voxel_trace.hip) indexes the grid with two 24-bit multiplies and a 32-bit byte
-// offset, exact only under these bounds.
+// Block grid limits (sfrt_voxel_set_blocks refuses larger grids): the reference's map key
+// (x << 20) + (y << 10) + z (World.cpp:385) addresses x < 2048, y, z < 1024 without overlap.
 constexpr int kVoxMaxX = 2048, kVoxMaxY = 1024, kVoxMaxZ = 1024;
-static_assert(kVoxMaxX <= (1 << 24) && kVoxMaxY <= (1 << 24) && kVoxMaxZ <= (1 << 24),
-              "v_mad_u32_u24 factors must be below 2^24");
-static_assert((long long)(kVoxMaxX - 1) * kVoxMaxY + (kVoxMaxY - 1) < (1ll << 24),
-              "cx * ny + cy is the second v_mad_u32_u24's 24-bit factor");
-static_assert((long long)kVoxMaxX * kVoxMaxY * kVoxMaxZ * 2 <= (1ll << 32),
-              "int16 cell byte offsets must fit in 32 bits");
+// On the device the world is the key-indexed byte array of cell_hit (voxel_trace.hip): byte
+// (x << 20) + (y << 10) + z holds id + kVoxCellBias for a block (ids are in (-kVoxSlots,
+// kVoxSlots)), 0 for no block; nx << 20 bytes, at most 2 GiB, so the buffer range fits an int.
+constexpr int kVoxCellBias = 10;
+static_assert(kVoxMaxY == 1024 && kVoxMaxZ == 1024, "the key's y and z fields are 10 bits");
+static_assert((long long)kVoxMaxX << 20 <= (1ll << 31), "byte offsets and the range fit 31 bits");
+static_assert(2 * (kVoxSlots - 1) + 1 <= 255, "a code fits a byte");
 
 struct VoxDyn {                             // struct Dynamic fields Raycast reads (World.h:25-38)
   float px, py, pz;
@@ -63,9 +62,8 @@ struct VoxFrame {
   int32_t sub_w, sub_row0, sub_rows;
   const float* col;                         // per column i: dir.x, dir.z, atan2f(dir.z, dir.x)
   const float* row;                         // per row j: dir.y, yscale
-  const int16_t* blocks;                    // dense [nx][ny][nz], textureID or kVoxEmpty
-  int32_t nx, ny, nz;
-  uint32_t grid_bytes;                      // nx * ny * nz * 2, at most 2^32 - 1 (buffer range)
+  const uint8_t* cells;                     // key-indexed codes (cell_hit), nx << 20 bytes
+  uint32_t cell_bytes;                      // nx << 20: the buffer range
   // The fast primary DDA's bound (sfrt_voxel.cpp dda_qlim): a ray whose direction
   // has max|d_k| <= dda_qlim * min|d_k| keeps every DDA position below 2^30 in magnitude, where
   // a plain v_cvt_i32_f32 equals to_i32; 0 sends every wave to the guarded DDA

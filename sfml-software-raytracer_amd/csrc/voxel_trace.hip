@@ -14,6 +14,12 @@
 
 #pragma clang fp contract(off)
 
+// cell_hit's buffer descriptor word 3 (0x00020000, DATA_FORMAT_32) is the gfx9 / CDNA encoding;
+// gfx10+ lay that word out differently.  This file is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "voxel_trace.hip: the grid's buffer descriptor is encoded for gfx950 (CDNA4)"
+#endif
+
 namespace sfrt {
 namespace {
 
@@ -45,29 +51,23 @@ struct V3 {
   float x, y, z;
 };
 
-// blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476): present iff the key is
-// non-negative and decodes to an occupied cell of the dense grid.  Branch-free: a negative key
-// has cx = key >> 20 (logical) >= 2048 >= nx, so three unsigned compares decide validity alone;
-// the index (cx * ny + cy) * nz + cz is computed for every lane and read through a buffer
-// resource over the grid (32-bit offset, hardware range check: an invalid lane's offset may
-// point anywhere and reads harmlessly) -- no exec-mask branches or 64-bit address arithmetic
-// around the per-step lookup (profiles/ab/r4_ab1, r4_ab4).
-// nx <= kVoxMaxX, ny <= kVoxMaxY, nz <= kVoxMaxZ (voxel_trace.h, static_asserts there): for a
-// valid cell every factor is below 2^24 and the index below 2^31, so two full-rate
-// v_mad_u32_u24 and a 32-bit byte offset are exact (left alone, the compiler turns the first
-// into a quarter-rate v_mad_u64_u32).  `id` is the cell's texture id when the cell is hit.
+// blocks.contains((x << 20) + (y << 10) + z) (World.cpp:385, 476).  The reference's map key IS
+// a linear index: (x << 20) + (y << 10) + z, in wrapping 32-bit arithmetic, is the offset of cell
+// (x, y, z) in a dense [2048][1024][1024] array, and every stored key lies below nx << 20.  So the
+// host stores the world as that array of bytes (VoxFrame::cells, nx << 20 bytes: code = id +
+// kVoxCellBias, 0 = empty; rows and planes beyond ny / nz stay 0), and a lookup is the key itself
+// as the byte offset of a buffer load whose range check (num_records = nx << 20) returns 0 for
+// every key at or past the last x-plane -- negative keys included (>= 2^31 as unsigned).  No
+// decode of the key, no validity compares, no index arithmetic: two v_lshl_add_u32 and the load
+// per step, exactly the reference's contains() (profiles/ab/r5_ab1).  `code` is the cell's code
+// when the cell is hit (id = code - kVoxCellBias).
 __device__ __forceinline__ bool cell_hit(const VoxFrame& f, int32_t x, int32_t y, int32_t z,
-                                         int16_t& id) {
+                                         uint32_t& code) {
   const uint32_t key = ((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z;
-  const uint32_t cx = key >> 20, cy = (key >> 10) & 1023u, cz = key & 1023u;
-  const bool valid = (cx < (uint32_t)f.nx) & (cy < (uint32_t)f.ny) & (cz < (uint32_t)f.nz);
-  uint32_t c;
-  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(cx), "s"((uint32_t)f.ny), "v"(cy));
-  __asm__("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(c) : "v"(c), "s"((uint32_t)f.nz), "v"(cz));
-  const __amdgpu_buffer_rsrc_t grid =
-      __builtin_amdgcn_make_buffer_rsrc((void*)f.blocks, (short)0, (int)f.grid_bytes, 0x00020000);
-  id = (int16_t)__builtin_amdgcn_raw_buffer_load_b16(grid, (int)(c * 2u), 0, 0);
-  return valid & (id != kVoxEmpty);
+  const __amdgpu_buffer_rsrc_t cells =
+      __builtin_amdgcn_make_buffer_rsrc((void*)f.cells, (short)0, (int)f.cell_bytes, 0x00020000);
+  code = __builtin_amdgcn_raw_buffer_load_b8(cells, (int)key, 0, 0);
+  return code != 0u;
 }
 
 __device__ __forceinline__ uint32_t texel(const VoxFrame& f, const VoxTex& t, uint32_t x,
@@ -129,10 +129,44 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
               yz = RECIP ? 1.0f / lz : 0.0f;
   const float m2 = maxDist * 2;
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
+#if SFRT_VOX_LLOOP
+  // One way out of the loop, as in raycast_t: the reference's loop test and its block hit
+  // (return false) become one stop condition at the bottom of the step, the cell of the next
+  // step's top tested there (only while the loop test holds, as the reference tests it).
+  bool blocked = false;
+  if ((0u < maxIter) & (dist < maxDist)) {
+    work++;
+    uint32_t code;
+    blocked = cell_hit(f, pix, piy, piz, code);
+    if (!blocked) {
+      for (uint32_t i = 0;;) {
+        const float a = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
+        const float b = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
+        const float c = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
+        float raySpeed = a;  // std::min({a, b, c})
+        if (b < raySpeed) raySpeed = b;
+        if (c < raySpeed) raySpeed = c;
+        raySpeed += 0.002f;
+        dist += raySpeed;
+        pos.x = pos.x + dir.x * raySpeed;
+        pos.y = pos.y + dir.y * raySpeed;
+        pos.z = pos.z + dir.z * raySpeed;
+        pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
+        i++;
+        const bool more = (i < maxIter) & (dist < maxDist);
+        work += more ? 1u : 0u;
+        blocked = more & cell_hit(f, pix, piy, piz, code);
+        if (!more | blocked) break;
+      }
+    }
+  }
+  return !blocked & (dist >= maxDist);
+}
+#else
   for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
     work++;
-    int16_t id;
-    if (cell_hit(f, pix, piy, piz, id)) return false;
+    uint32_t code;
+    if (cell_hit(f, pix, piy, piz, code)) return false;
     const float a = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
     const float b = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
     const float c = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
@@ -148,6 +182,7 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
   }
   return dist >= maxDist;
 }
+#endif
 
 __device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
                          uint32_t& work) {
@@ -161,7 +196,7 @@ __device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
 template <bool RECIP>
 __device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t pix, int32_t piy,
                                               int32_t piz, int colRay, float sx, float sy,
-                                              float sz, float dist, int16_t id, uint32_t& work) {
+                                              float sz, float dist, int id, uint32_t& work) {
   uint32_t c;
   if (id < 0) {
     c = f.colors[-id];
@@ -244,94 +279,102 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   // Shaded inside the loop, the light loop and its shadow rays ran once per distinct hit step
   // of the wave with the lanes of that step only (profiles/ab/r4_ab7: 4K 299 -> 289 us; with
   // the per-wave light skip 265 us).
-  bool hit = false;
-  int16_t hid = 0;
-  uint32_t early = 0u;
-  for (uint32_t i = 0; dist < f.view_distance && i < f.maxiter; i++) {
-    work++;
-    const float xray = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
-    const float yray = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
-    const float zray = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
-    // the reference's if / else-if / else (World.cpp:330-350) as selects: one branch-free step
-    // (as branches the compiler built an exec-mask diamond with ~12 scalar instructions).  In the
-    // fast DDA no ray is NaN (finite numerators over |d| >= 2^-60), so the reference's choice is
-    // the first axis whose ray equals the minimum (v_min3_f32; +-0 compare equal).  The speed
-    // can differ from the reference's only in the sign of a zero (a negative ray underflowing to
-    // -0 beside a +0 one), which reaches the position only through dir * speed added to a -0.0
-    // component (a -0.0 camera coordinate not yet moved), and no output depends on that sign
-    // (to_i32, the fractions, the texel and light offsets all map +-0 alike)
-    bool ax, ay;
-    float raySpeed;
-    if (RECIP) {
-      raySpeed = fminf(fminf(xray, yray), zray);
-      ax = xray == raySpeed;
-      ay = !ax & (yray == raySpeed);
-    } else {
-      ax = (xray <= yray) & (xray <= zray);
-      ay = !ax & (yray <= xray) & (yray <= zray);
-      raySpeed = ax ? xray : (ay ? yray : zray);
-    }
-    const float rs2 = raySpeed + 0.002f;
-    colRay = ax ? 1 : (ay ? 2 : 3);
-    const float tryDist = dist + raySpeed;
-
-    // dynamic billboards in front of the next block (World.cpp:353-378)
-    // the next billboard's distance is held in a register (NaN past the last), so the test
-    // reads no memory on the steps that pass no billboard (nearly all; it was a dependent
-    // global load at every step), and a wave whose lanes all pass none skips the loop
-    if (__builtin_amdgcn_ballot_w64(tryDist >= dnext)) {
-      V3 bp = pos;
-      float bdist = dist;
-      while (tryDist >= dnext) {
-      const VoxDyn& d = f.dyn[DI];
-      const float bs = d.dist - bdist;
-      bdist = d.dist;
-      bp.x = bp.x + dir.x * bs;
-      bp.y = bp.y + dir.y * bs;
-      bp.z = bp.z + dir.z * bs;
-      const float to = d.py - bp.y;
-      const float sizey = d.sy * yscale;
-      if (fabsf(to) < sizey) {
-        float ang = d.atan_b - atan_dir;  // VAngleXZ(dir, VNormalizeXZ(d->pos - cam.pos))
-        ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
-        ang = ang * bdist;
-        const VoxTex& t = f.dyn_tex[d.tex];
-        const float xf = (0.5f + ang / kPI * 0.5f / d.sx);
-        if (xf > 0 && xf < 1) {
-          int32_t x = to_i32(xf * (float)(uint32_t)t.w);
-          int32_t y = to_i32((sizey + to) / sizey / 2 * (float)(uint32_t)t.h);
-          x = x < 0 ? 0 : x;
-          y = y < 0 ? 0 : y;
-          const uint32_t c = texel(f, t, (uint32_t)x, (uint32_t)y);
-          if ((c >> 24) > 127u) {
-            early = pack(to_u8(min255((float)(c & 0xffu) * d.r)),
-                         to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
-                         to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
-            goto done;
+  //
+  // One way out of the step loop: the reference leaves World::Raycast's loop three ways (its
+  // loop test, a block hit, a billboard's opaque texel); as three divergent exits the compiler
+  // kept a lane mask per exit and merged EXEC around each, ~35 scalar instructions and 3
+  // branches per step (tools/isa_block_profile.py).  Here a lane computes one stop condition and
+  // leaves at the bottom of the step, its outcome in a register (0 = marched out, 1 = block, 2 =
+  // billboard): 4K 234.6 -> 208.7 us (profiles/ab/r5_ab1).  A lane stopped by a billboard still advances in that step: nothing of it is read
+  // afterwards but `early`.  The first loop test is uniform (dist = 0, i = 0).
+  uint32_t outcome = 0u, hcode = 0u, early = 0u;
+  if (0.0f < f.view_distance && 0u < f.maxiter) {
+    for (uint32_t i = 0;;) {
+      work++;
+      const float xray = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
+      const float yray = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
+      const float zray = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
+      // the reference's if / else-if / else (World.cpp:330-350) as selects: one branch-free
+      // step.  In the fast DDA no ray is NaN (finite numerators over |d| >= 2^-60), so the
+      // reference's choice is the first axis whose ray equals the minimum (v_min3_f32; +-0
+      // compare equal).  The speed can differ from the reference's only in the sign of a zero (a
+      // negative ray underflowing to -0 beside a +0 one), which reaches the position only through
+      // dir * speed added to a -0.0 component (a -0.0 camera coordinate not yet moved), and no
+      // output depends on that sign (to_i32, the fractions, the texel and light offsets all map
+      // +-0 alike)
+      bool ax, ay;
+      float raySpeed;
+      if (RECIP) {
+        raySpeed = fminf(fminf(xray, yray), zray);
+        ax = xray == raySpeed;
+        ay = !ax & (yray == raySpeed);
+      } else {
+        ax = (xray <= yray) & (xray <= zray);
+        ay = !ax & (yray <= xray) & (yray <= zray);
+        raySpeed = ax ? xray : (ay ? yray : zray);
+      }
+      const float rs2 = raySpeed + 0.002f;
+      colRay = ax ? 1 : (ay ? 2 : 3);
+      const float tryDist = dist + raySpeed;
+      // dynamic billboards in front of the next block (World.cpp:353-378): the next billboard's
+      // distance is held in a register (NaN past the last), so the test reads no memory on the
+      // steps that pass no billboard (nearly all), and a wave whose lanes all pass none skips
+      // the loop, which works on copies of pos and dist (the reference moves both there and then
+      // overwrites them with tryPos / tryDist)
+      uint32_t opaque = 0u;
+      if (__builtin_amdgcn_ballot_w64(tryDist >= dnext)) {
+        V3 bp = pos;
+        float bdist = dist;
+        while (tryDist >= dnext) {
+          const VoxDyn& d = f.dyn[DI];
+          const float bs = d.dist - bdist;
+          bdist = d.dist;
+          bp.x = bp.x + dir.x * bs;
+          bp.y = bp.y + dir.y * bs;
+          bp.z = bp.z + dir.z * bs;
+          const float to = d.py - bp.y;
+          const float sizey = d.sy * yscale;
+          if (fabsf(to) < sizey) {
+            float ang = d.atan_b - atan_dir;  // VAngleXZ(dir, VNormalizeXZ(d->pos - cam.pos))
+            ang = ang > kPI ? ang - kPI2 : (ang < -kPI ? ang + kPI2 : ang);
+            ang = ang * bdist;
+            const VoxTex& t = f.dyn_tex[d.tex];
+            const float xf = (0.5f + ang / kPI * 0.5f / d.sx);
+            if (xf > 0 && xf < 1) {
+              int32_t x = to_i32(xf * (float)(uint32_t)t.w);
+              int32_t y = to_i32((sizey + to) / sizey / 2 * (float)(uint32_t)t.h);
+              x = x < 0 ? 0 : x;
+              y = y < 0 ? 0 : y;
+              const uint32_t c = texel(f, t, (uint32_t)x, (uint32_t)y);
+              if ((c >> 24) > 127u) {
+                early = pack(to_u8(min255((float)(c & 0xffu) * d.r)),
+                             to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
+                             to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
+                opaque = 1u;
+                break;
+              }
+            }
           }
+          DI++;
+          dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf("");
         }
       }
-      DI++;
-      dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf("");
-      }
-    }
-
-    dist = tryDist;
-    pos.x += dir.x * (ax ? rs2 : raySpeed);  // tryPos (World.cpp:330-350)
-    pos.y += dir.y * (ay ? rs2 : raySpeed);
-    pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
-    pix = pos_i32<RECIP>(pos.x); piy = pos_i32<RECIP>(pos.y); piz = pos_i32<RECIP>(pos.z);
-    int16_t id;
-    if (cell_hit(f, pix, piy, piz, id)) {  // hit a block (World.cpp:385)
-      hit = true;
-      hid = id;
-      break;
+      dist = tryDist;
+      pos.x += dir.x * (ax ? rs2 : raySpeed);  // tryPos (World.cpp:330-350)
+      pos.y += dir.y * (ay ? rs2 : raySpeed);
+      pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
+      pix = pos_i32<RECIP>(pos.x); piy = pos_i32<RECIP>(pos.y); piz = pos_i32<RECIP>(pos.z);
+      const bool h = cell_hit(f, pix, piy, piz, hcode);  // hit a block (World.cpp:385)
+      outcome = opaque ? 2u : (h ? 1u : 0u);
+      i++;
+      if (outcome | !(dist < f.view_distance) | !(i < f.maxiter)) break;
     }
   }
-  if (hit) return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist, hid, work);
+  if (outcome == 2u) return early;
+  if (outcome == 1u)
+    return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist,
+                            (int)hcode - kVoxCellBias, work);
   return pack(0, 0, 0, 255);  // sf::Color::Black
-done:
-  return early;
 }
 
 __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
@@ -408,7 +451,7 @@ int launch_voxel(const VoxFrame& f, void* stream) {
   if (voxel_tile_key(f, &tiles) == 0) return 0;
   // the kernel reads the grid through a buffer resource over f.blocks and the tables
   // unguarded: refuse a record whose device pointers were not filled
-  if (!f.blocks || f.grid_bytes == 0 || !f.col || !f.row || !f.out || !f.status ||
+  if (!f.cells || f.cell_bytes == 0 || !f.col || !f.row || !f.out || !f.status ||
       (f.ndyn > 0 && !f.dyn) || (f.nlights > 0 && !f.lights))
     return -1;
   if (tiles > 0x7ffffffeLL) return -1;
