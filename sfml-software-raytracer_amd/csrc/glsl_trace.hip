@@ -102,7 +102,6 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   // (host-checked with the same test), so they change nothing; a whole pass
   // in which no lane of the wave is inside a wall leaves the state at a fixed
   // point, so the remaining passes would repeat it and are skipped.
-#if SFRT_GLSL_LOOPS
   // The passes as an outer loop and the walls as a counted inner loop (the record address
   // stepped, not recomputed): the single loop with its wrap-around index kept ~20 scalar
   // instructions per wall visit (tools/isa_block_profile.py).
@@ -133,39 +132,6 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
       if (!moved) break;  // uniform: a pass in which no lane moved is a fixed point
     }
   }
-#else
-  bool moved = false;
-  for (int j = f.wall_start, k = f.wall_start % (f.sc > 0 ? f.sc : 1); j < 3 * f.sc; j++) {
-    const GlslWall w = ld(walls, k);
-    const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
-    const float s = (rx * rx + ry * ry) + rz * rz;
-    const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
-    // A wave with no lane inside skips the body: every lane's tosurf would be +0 (the uniforms
-    // are bounded, so (...) is finite and >= 0) and pos + dir * +0 == pos unless a component
-    // is -0.0, which pos holds only if campos does (x + y == -0 needs both -0): then the body
-    // runs for every iteration (cam_negzero, host-set), as the shader does.  One update path,
-    // so the loop-carried position needs no register copies on the skipping iterations.
-    const uint64_t inside_mask = __builtin_amdgcn_ballot_w64(inside);  // scalar tests only
-    if ((inside_mask | (uint64_t)(uint32_t)f.cam_negzero) != 0) {
-      moved |= inside_mask != 0;
-      const float cs = inside ? 1.0f : 0.0f;
-      const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
-      const float c = cs * s - w.rr;
-      const float tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
-      px = px + dx * tosurf;
-      py = py + dy * tosurf;
-      pz = pz + dz * tosurf;
-      total = total + tosurf;
-    }
-    draw = inside ? k : draw;
-    if (++k == f.sc) {
-      k = 0;
-      if (!moved) break;  // uniform
-      moved = false;
-    }
-  }
-
-#endif
 
   // ---- metaball march over lights + ospheres (:87-112) ----
   const int nballs = f.all - f.sc;
@@ -174,62 +140,53 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   int closest = 0;
   float snx = 0.0f, sny = 0.0f, snz = 0.0f;
   int steps = 0;
-#if SFRT_GLSL_LOOPS
   // One way out of the march: the shader's loop test and our step cap as one condition at the
   // bottom (the cap's status after the loop): two divergent exits cost a lane mask merge each.
+  // With the wall passes' loop split (above): 4K 455.8 -> 435.3 us (profiles/ab/r5_ab3).  The
+  // ball records loaded one ball ahead (two register sets, an empty asm statement placing each
+  // wait before the next issue) measured slower: 464.7 us (same A/B).
   if (ball_dist < total && smooth > 0.01f) {
-  for (;;) {
-    ++steps;
-#else
-  while (ball_dist < total && smooth > 0.01f) {
-    if (++steps > kGlslMarchCap) {
-      atomicOr(f.status, 1);
-      break;
+    for (;;) {
+      ++steps;
+      const float tx = cx + dx * ball_dist, ty = cy + dy * ball_dist, tz = cz + dz * ball_dist;
+      smooth = 999999999.0f;
+      closest = 0;
+      float shortest = 9999999.0f;
+      snx = sny = snz = 0.0f;
+      // Dominance threshold (t*(1+1e-5) + 1e-4)*(1+6e-6), t = max(smooth + 0.5, shortest, 0.5),
+      // rounded up (kThrMul, kThrAdd); it only changes when a ball's body runs.
+      float thr = 1e30f;
+      for (int k = 0; k < nballs; k++) {
+        const GlslBall b = ld(balls, k);
+        const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
+        // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
+        // margin), polsmin returns smooth, closest/shortest keep their values and
+        // normalFactor == 1, so the body changes nothing (smoothNormal at most
+        // flips the sign of a zero component, which no output depends on).
+        // The test is ours, not the shader's: the squared length by two fmas and both bounds
+        // inflated by (1+6e-6) (r_skip on the host, thr here), which implies the round-3 test
+        // ss >= (r + t*(1+1e-5) + 1e-4)^2 * (1+1e-5) on the shader's own ss.
+        const float ssf = __builtin_fmaf(ox, ox, __builtin_fmaf(oy, oy, oz * oz));
+        const float bnd = b.r_skip + thr;
+        const bool dominated = ssf >= bnd * bnd;
+        if (!__builtin_amdgcn_ballot_w64(!dominated)) continue;
+        const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100
+        const float other = sqrt_cr(ss) - b.r;
+        const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
+        smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
+        closest = other < shortest ? f.sc + k : closest;                  // :105
+        shortest = gmin(shortest, other);
+        const float nf = gclamp(other, 0.0f, 0.5f) * 2.0f;
+        snx = nf * snx - (1.0f - nf) * ox;
+        sny = nf * sny - (1.0f - nf) * oy;
+        snz = nf * snz - (1.0f - nf) * oz;
+        thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
+      }
+      ball_dist += smooth + 0.01f;
+      if (!((ball_dist < total) & (smooth > 0.01f) & (steps < kGlslMarchCap))) break;
     }
-#endif
-    const float tx = cx + dx * ball_dist, ty = cy + dy * ball_dist, tz = cz + dz * ball_dist;
-    smooth = 999999999.0f;
-    closest = 0;
-    float shortest = 9999999.0f;
-    snx = sny = snz = 0.0f;
-    // Dominance threshold (t*(1+1e-5) + 1e-4)*(1+6e-6), t = max(smooth + 0.5, shortest, 0.5),
-    // rounded up (kThrMul, kThrAdd); it only changes when a ball's body runs.
-    float thr = 1e30f;
-    for (int k = 0; k < nballs; k++) {
-      const GlslBall b = ld(balls, k);
-      const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
-      // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
-      // margin), polsmin returns smooth, closest/shortest keep their values and
-      // normalFactor == 1, so the body changes nothing (smoothNormal at most
-      // flips the sign of a zero component, which no output depends on).
-      // The test is ours, not the shader's: the squared length by two fmas and both bounds
-      // inflated by (1+6e-6) (r_skip on the host, thr here), which implies the round-3 test
-      // ss >= (r + t*(1+1e-5) + 1e-4)^2 * (1+1e-5) on the shader's own ss.
-      const float ssf = __builtin_fmaf(ox, ox, __builtin_fmaf(oy, oy, oz * oz));
-      const float bnd = b.r_skip + thr;
-      const bool dominated = ssf >= bnd * bnd;
-      if (!__builtin_amdgcn_ballot_w64(!dominated)) continue;
-      const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100
-      const float other = sqrt_cr(ss) - b.r;
-      const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
-      smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
-      closest = other < shortest ? f.sc + k : closest;                  // :105
-      shortest = gmin(shortest, other);
-      const float nf = gclamp(other, 0.0f, 0.5f) * 2.0f;
-      snx = nf * snx - (1.0f - nf) * ox;
-      sny = nf * sny - (1.0f - nf) * oy;
-      snz = nf * snz - (1.0f - nf) * oz;
-      thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
-    }
-    ball_dist += smooth + 0.01f;
-#if SFRT_GLSL_LOOPS
-    if (!((ball_dist < total) & (smooth > 0.01f) & (steps < kGlslMarchCap))) break;
+    if (steps == kGlslMarchCap && ball_dist < total && smooth > 0.01f) atomicOr(f.status, 1);
   }
-  if (steps == kGlslMarchCap && ball_dist < total && smooth > 0.01f) atomicOr(f.status, 1);
-  }
-#else
-  }
-#endif
   work = (uint32_t)steps;
 
   // ---- wall or ball (:114-120) ----

@@ -226,8 +226,11 @@ struct sfrt_voxel {
     std::vector<sfrt::VoxLight> vl(lights.size());
     for (size_t k = 0; k < lights.size(); k++) {
       const sfrt_light& L = lights[k];
-      vl[k] = {L.pos[0], L.pos[1], L.pos[2], L.intensity, L.r, L.g, L.b, L.shadows,
-               light_dd_skip(light_dd_pass(L.intensity))};
+      sfrt::VoxLight& o = vl[k];
+      o.px = L.pos[0]; o.py = L.pos[1]; o.pz = L.pos[2];
+      o.dd_skip = light_dd_skip(light_dd_pass(L.intensity));
+      o.intensity = L.intensity; o.r = L.r; o.g = L.g; o.b = L.b;
+      o.shadows = L.shadows;
     }
     // one blob per launch: col | row | dyn | lights, 16-byte aligned parts
     auto up16 = [](size_t b) { return (b + 15) & ~(size_t)15; };

@@ -38,15 +38,16 @@ struct VoxDyn {                             // struct Dynamic fields Raycast rea
 
 struct VoxLight {                           // struct Light (World.h:40-47)
   float px, py, pz;
-  float intensity, r, g, b;
-  int32_t shadows;
   // Squared distances dd >= dd_pass have intensity / dd - dd * 0.002f <= 0 in binary32
   // (World.cpp:425-426: the light adds nothing there): dd_pass is the smallest such float, found
   // on the host by bisection over the bit patterns (the test is monotone in dd; 0 when no dd
   // passes).  The kernel's per-wave skip tests the fma-evaluated squared distance, within
   // 6 ulp (relative 2^-20) of the reference's, against dd_skip = RU(dd_pass / (1 - 2^-20)):
-  // ddf >= dd_skip implies dd >= dd_pass.
+  // ddf >= dd_skip implies dd >= dd_pass.  Beside the position, so that the skip test's four
+  // dwords are one scalar load.
   float dd_skip;
+  float intensity, r, g, b;
+  int32_t shadows;
 };
 
 struct VoxTex {

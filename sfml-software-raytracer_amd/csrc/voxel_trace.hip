@@ -129,7 +129,6 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
               yz = RECIP ? 1.0f / lz : 0.0f;
   const float m2 = maxDist * 2;
   const uint32_t maxIter = to_u32(m2 < 20.0f ? 20.0f : m2);
-#if SFRT_VOX_LLOOP
   // One way out of the loop, as in raycast_t: the reference's loop test and its block hit
   // (return false) become one stop condition at the bottom of the step, the cell of the next
   // step's top tested there (only while the loop test holds, as the reference tests it).
@@ -162,27 +161,6 @@ __device__ bool lraycast_t(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
   }
   return !blocked & (dist >= maxDist);
 }
-#else
-  for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {
-    work++;
-    uint32_t code;
-    if (cell_hit(f, pix, piy, piz, code)) return false;
-    const float a = dv<RECIP>(dda_num(dirxadd, sx, pos.x, pix), lx, yx);
-    const float b = dv<RECIP>(dda_num(diryadd, sy, pos.y, piy), ly, yy);
-    const float c = dv<RECIP>(dda_num(dirzadd, sz, pos.z, piz), lz, yz);
-    float raySpeed = a;  // std::min({a, b, c})
-    if (b < raySpeed) raySpeed = b;
-    if (c < raySpeed) raySpeed = c;
-    raySpeed += 0.002f;
-    dist += raySpeed;
-    pos.x = pos.x + dir.x * raySpeed;
-    pos.y = pos.y + dir.y * raySpeed;
-    pos.z = pos.z + dir.z * raySpeed;
-    pix = to_i32(pos.x); piy = to_i32(pos.y); piz = to_i32(pos.z);
-  }
-  return dist >= maxDist;
-}
-#endif
 
 __device__ bool lraycast(const VoxFrame& f, V3 pos, V3 dir, float maxDist,
                          uint32_t& work) {
@@ -218,8 +196,11 @@ __device__ __forceinline__ uint32_t shade_hit(const VoxFrame& f, V3 pos, int32_t
   const float l0 = 0.05f / dist - dist * 0.0001f;
   float litr = l0 < 0.0f ? 0.0f : l0;
   float litg = litr, litb = litr;
-  for (int j = 0; j < f.nlights; j++) {
-    const VoxLight L = light_at(f.lights, j);
+  // the record address stepped (a j * 36 product per light was four scalar instructions) and
+  // the skip test's fields one scalar load (VoxLight): 4K 201.5 -> 198.0 us (profiles/ab/r5_ab2)
+  const VoxLight* const lend = f.lights + f.nlights;
+  for (const VoxLight* lp = f.lights; lp != lend; ++lp) {
+    const VoxLight L = light_at(lp, 0);
     const float ex = pos.x - L.px, ey = pos.y - L.py, ez = pos.z - L.pz;
     // dd >= dd_pass: the light adds nothing (host threshold, exact); a wave none of whose lanes
     // is that close skips the light's division and the rest.  The test is ours: the squared
@@ -280,14 +261,19 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   // of the wave with the lanes of that step only (profiles/ab/r4_ab7: 4K 299 -> 289 us; with
   // the per-wave light skip 265 us).
   //
+  //
   // One way out of the step loop: the reference leaves World::Raycast's loop three ways (its
   // loop test, a block hit, a billboard's opaque texel); as three divergent exits the compiler
   // kept a lane mask per exit and merged EXEC around each, ~35 scalar instructions and 3
-  // branches per step (tools/isa_block_profile.py).  Here a lane computes one stop condition and
-  // leaves at the bottom of the step, its outcome in a register (0 = marched out, 1 = block, 2 =
-  // billboard): 4K 234.6 -> 208.7 us (profiles/ab/r5_ab1).  A lane stopped by a billboard still advances in that step: nothing of it is read
-  // afterwards but `early`.  The first loop test is uniform (dist = 0, i = 0).
-  uint32_t outcome = 0u, hcode = 0u, early = 0u;
+  // branches per step (tools/isa_block_profile.py).  Here a lane tests one stop condition at the
+  // bottom of the step, and what stopped it is read from registers afterwards: `early` != 0 (a
+  // billboard's texel, alpha > 127), else `hcode` != 0 (the cell code of a block), else it marched
+  // out.  A lane stopped by a billboard still advances in that step; nothing of it but `early` is
+  // read afterwards.  The first loop test is uniform (dist = 0, i = 0).  4K 234.6 -> 208.7 us, and
+  // 208.0 -> 201.5 with the outcome read back this way and colRay kept in the loop (the empty asm
+  // below: sunk past the loop, the axis choice carried two lane masks merged with EXEC every step)
+  // (profiles/ab/r5_ab1, r5_ab2).
+  uint32_t hcode = 0u, early = 0u;
   if (0.0f < f.view_distance && 0u < f.maxiter) {
     for (uint32_t i = 0;;) {
       work++;
@@ -321,7 +307,6 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       // steps that pass no billboard (nearly all), and a wave whose lanes all pass none skips
       // the loop, which works on copies of pos and dist (the reference moves both there and then
       // overwrites them with tryPos / tryDist)
-      uint32_t opaque = 0u;
       if (__builtin_amdgcn_ballot_w64(tryDist >= dnext)) {
         V3 bp = pos;
         float bdist = dist;
@@ -350,7 +335,6 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
                 early = pack(to_u8(min255((float)(c & 0xffu) * d.r)),
                              to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
                              to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
-                opaque = 1u;
                 break;
               }
             }
@@ -364,14 +348,14 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       pos.y += dir.y * (ay ? rs2 : raySpeed);
       pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
       pix = pos_i32<RECIP>(pos.x); piy = pos_i32<RECIP>(pos.y); piz = pos_i32<RECIP>(pos.z);
-      const bool h = cell_hit(f, pix, piy, piz, hcode);  // hit a block (World.cpp:385)
-      outcome = opaque ? 2u : (h ? 1u : 0u);
+      __asm__ volatile("" : "+v"(colRay));  // keeps the axis choice a register of the loop
+      cell_hit(f, pix, piy, piz, hcode);  // hcode != 0: hit a block (World.cpp:385)
       i++;
-      if (outcome | !(dist < f.view_distance) | !(i < f.maxiter)) break;
+      if ((early != 0u) | (hcode != 0u) | !(dist < f.view_distance) | !(i < f.maxiter)) break;
     }
   }
-  if (outcome == 2u) return early;
-  if (outcome == 1u)
+  if (early != 0u) return early;  // a billboard's texel with alpha > 127: never 0
+  if (hcode != 0u)
     return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist,
                             (int)hcode - kVoxCellBias, work);
   return pack(0, 0, 0, 255);  // sf::Color::Black

@@ -407,6 +407,36 @@ def test_march_dominance_test_implies_round3_test():
 
 
 @pytest.mark.gpu
+def test_gpu_tables_reused_across_streams(shader, floor):
+    """ADVICE r4 (sfrt_host.h TableSlot): per-draw tables staged on stream A behind queued work,
+    then reused at once by a draw on stream B with no host sync between: B must wait for A's
+    staging copy and draw the new uniforms."""
+    import torch
+    w, h = 320, 180
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for k in range(3):
+        u = gs.default_uniforms(w, h, 0.6 + 0.3 * k, 0.1, frames=5 + k)
+        shader.set_uniforms(u)
+        ba = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        bb = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(a):
+            torch.cuda._sleep(40_000_000)  # ~20 ms of queued work ahead of A's staging copy
+        shader.draw(ba.data_ptr(), w, h, w * 4, 0, h, a.cuda_stream)   # stages on A
+        shader.draw(bb.data_ptr(), w, h, w * 4, 0, h, b.cuda_stream)   # reuses on B at once
+        outs.append((u, ba, bb))
+    torch.cuda.synchronize()
+    shader.check(a.cuda_stream)
+    shader.check(b.cuda_stream)
+    for u, ba, bb in outs:
+        want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+        got_a, got_b = ba.cpu().numpy().ravel(), bb.cpu().numpy().ravel()
+        assert np.array_equal(got_a, want), first_diff(got_a, want, w)
+        assert np.array_equal(got_b, want), first_diff(got_b, want, w)
+
+
+@pytest.mark.gpu
 def test_gpu_tables_restaged_after_every_uniform_setter(shader, floor):
     """The per-draw tables (walls, balls, light/shadow pairs, materials) are staged once and
     reused while the uniforms do not change (sfrt_glsl.cpp u_version): a repeated draw equals

@@ -153,6 +153,42 @@ def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
 
 
 @pytest.mark.gpu
+def test_voxel_tables_reused_across_streams(vworld, assets):
+    """ADVICE r4 (sfrt_host.h TableSlot): tables staged on stream A behind queued work, then
+    reused at once by a frame on stream B, with no host sync between: B's frame must wait for
+    A's staging copy (hipStreamWaitEvent on the slot's event) and show the new scene, and the
+    slot's event must then cover both users before it is restaged."""
+    import dataclasses
+    import torch
+    w, h = 320, 180
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    base = vs.default_world((20.5, 2.2, 40.5), 1.0, 0.1)
+    vworld.set_scene(base, w, h)
+    buf0 = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+    vworld.render_band(buf0.data_ptr(), w * 4, 0, h, a.cuda_stream)
+    vworld.check(a.cuda_stream)
+    scenes_ = []
+    for k in range(3):  # three scene changes: each stages a new slot on A, read at once on B
+        sc = dataclasses.replace(base, cam_pos=(20.5 + 0.75 * (k + 1), 2.2, 40.5), rotation=1.0 + 0.2 * k)
+        vworld.set_scene(sc, w, h)
+        ba = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        bb = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(a):
+            torch.cuda._sleep(40_000_000)  # ~20 ms of queued work ahead of A's staging copy
+        vworld.render_band(ba.data_ptr(), w * 4, 0, h, a.cuda_stream)   # stages on A
+        vworld.render_band(bb.data_ptr(), w * 4, 0, h, b.cuda_stream)   # reuses on B at once
+        scenes_.append((sc, ba, bb))
+    torch.cuda.synchronize()
+    vworld.check(a.cuda_stream)
+    vworld.check(b.cuda_stream)
+    for sc, ba, bb in scenes_:
+        want = oracle.VoxelOracle(sc, w, h, assets[0], assets[1], vs.COLORS).render(host_threads())
+        assert np.array_equal(ba.cpu().numpy().ravel(), want)
+        assert np.array_equal(bb.cpu().numpy().ravel(), want)
+
+
+@pytest.mark.gpu
 def test_voxel_tables_restaged_after_every_setter(vworld, assets):
     """The per-frame tables (columns, rows, billboards, lights) are staged once and reused
     while nothing they depend on changes (sfrt_voxel.cpp tables_version): each setter alone --

@@ -456,8 +456,8 @@ def regions_voxel(blocks):
         "main_loop": "const float tryDist = dist + raySpeed;",
         "billboard_first": "V3 bp = pos;",
         "billboard_last": "dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf(\"\");\n        }",
-        "light_loop": "for (int j = 0; j < f.nlights; j++) {",
-        "shadow_loop": "for (uint32_t i = 0; i < maxIter && dist < maxDist; i++) {",
+        "light_loop": "const VoxLight L = light_at(lp, 0);",
+        "shadow_loop": "raySpeed += 0.002f;",
         "light_skip": "if (!__builtin_amdgcn_ballot_w64(ddf < L.dd_skip)) continue;",
     }.items()}
     lp = Loops(blocks)
