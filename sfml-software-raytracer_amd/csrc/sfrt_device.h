@@ -15,7 +15,7 @@ namespace sfrt {
 // the compiler if-converts such branches -- computing BOTH the fallback and the fast path
 // for every wave and selecting -- which cost ~5 % of the frame kernel's VALU.
 __device__ __forceinline__ float keep_branch(float v) {
-  __asm__ volatile("" : "+v"(v));
+  __asm__ volatile("; keep_branch" : "+v"(v));  // (the comment marks rare paths for tools/)
   return v;
 }
 

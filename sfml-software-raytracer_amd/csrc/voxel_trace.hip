@@ -348,7 +348,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       pos.y += dir.y * (ay ? rs2 : raySpeed);
       pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
       pix = pos_i32<RECIP>(pos.x); piy = pos_i32<RECIP>(pos.y); piz = pos_i32<RECIP>(pos.z);
-      __asm__ volatile("" : "+v"(colRay));  // keeps the axis choice a register of the loop
+      __asm__ volatile("; colRay" : "+v"(colRay));  // keeps the axis choice a loop register
       cell_hit(f, pix, piy, piz, hcode);  // hcode != 0: hit a block (World.cpp:385)
       i++;
       if ((early != 0u) | (hcode != 0u) | !(dist < f.view_distance) | !(i < f.maxiter)) break;

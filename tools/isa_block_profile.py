@@ -25,7 +25,7 @@ unmodified assembly) and prints, per launch size, the predicted VALU / SALU / SM
 branch instructions per wave next to the PMC pass's SQ_INSTS_* / SQ_WAVES, and a VALU and SALU
 attribution by source region (each instruction's region from its inline chain,
 llvm-symbolizer --inlining on the code object of the unmodified assembly, and the ISA loop it
-sits in).  Unlike tools/voxel_block_profile.py and glsl_block_profile.py (source-level counters
+sits in).  Unlike round 4's tools/voxel_block_profile.py and glsl_block_profile.py (source-level counters
 that charge a region's whole static code to every execution, 1.29x and 1.036x over PMC in round
 4) the totals here are exact by construction: they should equal PMC to the counters' noise.
 """
@@ -83,7 +83,7 @@ def parse_blocks(lines, symbol):
     """Basic blocks of `symbol` in order: dict(start = index of the first line after the block's
     label, name, header, parent, insts = [(line index, instruction text)], rare)."""
     st, en = function_range(lines, symbol)
-    blocks, cur, prev_asm = [], None, False
+    blocks, cur = [], None
     for i in range(st + 1, en):
         line = lines[i]
         m = re.match(r"^(\.LBB\d+_\d+):(.*)", line) or re.match(r"^; (%bb\.\d+):(.*)", line)
@@ -111,9 +111,8 @@ def parse_blocks(lines, symbol):
         if m:
             continue
         t = line.strip()
-        if t == ";;#ASMEND" and prev_asm:
-            cur["rare"] = True  # keep_branch(): an empty asm statement marks a rare fallback
-        prev_asm = t == ";;#ASMSTART"
+        if t == "; keep_branch":
+            cur["rare"] = True  # keep_branch() (sfrt_device.h): its asm comment marks a rare path
         if is_inst(line):
             cur["insts"].append((i, t.split(";")[0].strip()))
     return [b for b in blocks if b["insts"] or b["name"] != "entry"]
@@ -493,10 +492,10 @@ def regions_voxel(blocks):
 
 
 def regions_glsl(blocks):
-    """The blocks of tools/glsl_block_profile.py: by the ISA loop and the line of fragment()."""
+    """The regions of round 4's source-level GLSL tool: by the ISA loop and the line of fragment()."""
     A = {k: src_anchor("glsl", v) for k, v in {
         "wall_loop": "const bool inside = s <= w.s_in;",
-        "wall_inside_first": "moved |= inside_mask != 0;",
+        "wall_inside_first": "moved |= inside_mask;",
         "wall_inside_last": "total = total + tosurf;",
         "march_loop": "ball_dist += smooth + 0.01f;",
         "ball_loop": "const bool dominated = ssf >= bnd * bnd;",
