@@ -53,6 +53,10 @@ struct GlslFrame {
   int32_t sc, lc, all;
   int32_t cam_negzero;                 // a campos component is -0.0 (wall pass, below)
   int32_t wall_start;                  // first wall-pass iteration that can change a lane
+  // The per-wave wall cull's distance margin (glsl_trace.hip wall_mask): 1e-3 of the largest
+  // coordinate the wall pass can reach, + 1e-4; 0 disables the cull (a -0.0 in campos, more than
+  // 64 walls, non-finite bounds)
+  float wall_cull_margin;
   int32_t width, height, row0, rows, tiles_x;
   const GlslWall* walls;
   const GlslBall* balls;               // all - sc entries (lights, then ospheres)

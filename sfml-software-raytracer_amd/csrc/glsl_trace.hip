@@ -75,6 +75,59 @@ __device__ __forceinline__ T ld(const_ptr<T> p, int i) {
 // host inflates r_skip by the same (1 + 6e-6), rounding up (sfrt_glsl.cpp).
 constexpr float kThrMul = 0x1.00010ep+0f, kThrAdd = 0x1.a36ed4p-14f;
 
+// The walls the wave's rays can meet (bit k: wall k; sc <= 64, all 64 lanes active).  Every
+// position of the wall pass lies on its lane's ray campos + d t (t >= 0) up to the binary32 drift
+// of its few moves, and a lane can be inside wall k only within r_k of its centre; so when the
+// centre is farther than r_k + margin from every ray of the wave, `inside` is false for every
+// lane at every visit of wall k, whose body the loop skips anyway, and leaving the wall out of the
+// passes changes nothing.  The rays lie in a cone around the axis through the
+// tile's first and last lanes' rays: its half-angle's sine is the wave's largest |d x a| plus
+// slack.  The centre's distance from the cone's rays is |w| sin(alpha - theta) for alpha > theta
+// (alpha the angle of w = c - campos from the axis), |w| when alpha - theta >= 90 degrees (the
+// apex is nearest), 0 inside the cone.  A wave whose rays spread past 60 degrees keeps all walls.
+// margin = f.wall_cull_margin (host: 1e-3 of the largest coordinate the pass can reach, + 1e-4),
+// far above the positions' drift (< 4e-6 of it) and this test's own rounding.
+__device__ __forceinline__ uint64_t wall_mask(const GlslFrame& f, float dx, float dy, float dz) {
+  const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  float ax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), 0)) +
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), 63));
+  float ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), 0)) +
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dy), 63));
+  float az = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), 0)) +
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), 63));
+  const float al = __builtin_amdgcn_sqrtf((ax * ax + ay * ay) + az * az);
+  if (!(al > 0.5f)) return ~0ull;  // the corner rays more than 120 degrees apart: no cull
+  const float ia = 1.0f / al;
+  ax *= ia; ay *= ia; az *= ia;
+  // the largest |d x a| over the wave (bit patterns of non-negative floats), and every ray within
+  // 60 degrees of the axis (d . a >= 0.5)
+  const float cx = dy * az - dz * ay, cy = dz * ax - dx * az, cz = dx * ay - dy * ax;
+  const float s2 = (cx * cx + cy * cy) + cz * cz;
+  const bool wide = (dx * ax + dy * ay) + dz * az < 0.5f;
+  if (__builtin_amdgcn_ballot_w64(wide)) return ~0ull;
+  const float sin_t = __builtin_amdgcn_sqrtf(__uint_as_float(wave_max_u32(__float_as_uint(s2)))) + 1e-5f;
+  if (!(sin_t < 0.87f)) return ~0ull;
+  const float cos_t = __builtin_amdgcn_sqrtf(1.0f - sin_t * sin_t);
+  bool keep = true;
+  if (lane < f.sc) {
+    const GlslWall w = f.walls[lane];
+    const float wx = w.x - f.campos[0], wy = w.y - f.campos[1], wz = w.z - f.campos[2];
+    const float wl = __builtin_amdgcn_sqrtf((wx * wx + wy * wy) + wz * wz);
+    const float reach = w.r + f.wall_cull_margin;
+    if (wl >= reach) {  // else the camera is within reach of the wall: kept
+      const float ca = ((wx * ax + wy * ay) + wz * az) / wl;                  // cos alpha
+      const float qx = wy * az - wz * ay, qy = wz * ax - wx * az, qz = wx * ay - wy * ax;
+      const float sa = __builtin_amdgcn_sqrtf((qx * qx + qy * qy) + qz * qz) / wl;  // sin alpha
+      const float s_at = sa * cos_t - ca * sin_t;   // sin(alpha - theta)
+      const float c_at = ca * cos_t + sa * sin_t;   // cos(alpha - theta)
+      const float dist = s_at <= 0.0f ? 0.0f : (c_at <= 0.0f ? wl : wl * s_at);
+      keep = dist < reach;
+    }
+  }
+  return __builtin_amdgcn_ballot_w64(keep);
+}
+
+template <bool CULL>
 __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall> walls,
                                          const_ptr<GlslBall> balls, int i, int row,
                                          uint32_t& work, bool store = true) {
@@ -105,29 +158,46 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
   // The passes as an outer loop and the walls as a counted inner loop (the record address
   // stepped, not recomputed): the single loop with its wrap-around index kept ~20 scalar
   // instructions per wall visit (tools/isa_block_profile.py).
-  if (f.sc > 0) {
+  auto wall_visit = [&](int k, uint64_t& moved) {
+    const GlslWall w = ld(walls, k);
+    const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
+    const float s = (rx * rx + ry * ry) + rz * rz;
+    const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
+    const uint64_t inside_mask = __builtin_amdgcn_ballot_w64(inside);  // scalar tests only
+    if ((inside_mask | (uint64_t)(uint32_t)f.cam_negzero) != 0) {
+      moved |= inside_mask;
+      const float cs = inside ? 1.0f : 0.0f;
+      const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
+      const float c = cs * s - w.rr;
+      const float tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
+      px = px + dx * tosurf;
+      py = py + dy * tosurf;
+      pz = pz + dz * tosurf;
+      total = total + tosurf;
+    }
+    draw = inside ? k : draw;
+  };
+  if (CULL && f.sc > 0 && f.sc <= 64 && f.wall_cull_margin > 0.0f) {
+    // only the walls the wave's rays can meet, in index order (wall_mask above): at 4K each
+    // 8x8 tile's rays meet 2.4 of the default scene's 10 walls
+    const uint64_t wm = wall_mask(f, dx, dy, dz) & (f.sc == 64 ? ~0ull : ((1ull << f.sc) - 1ull));
+    int k0 = f.wall_start % f.sc;
+    for (int pass = f.wall_start / f.sc; pass < 3; pass++) {
+      uint64_t moved = 0;
+      uint64_t todo = wm & (~0ull << k0);
+      while (todo) {
+        const int k = (int)__builtin_ctzll(todo);
+        todo &= todo - 1ull;
+        wall_visit(k, moved);
+      }
+      k0 = 0;
+      if (!moved) break;  // uniform: a pass in which no lane moved is a fixed point
+    }
+  } else if (f.sc > 0) {
     int k = f.wall_start % f.sc;
     for (int pass = f.wall_start / f.sc; pass < 3; pass++) {
       uint64_t moved = 0;
-      for (; k < f.sc; k++) {
-        const GlslWall w = ld(walls, k);
-        const float rx = px - w.x, ry = py - w.y, rz = pz - w.z;
-        const float s = (rx * rx + ry * ry) + rz * rz;
-        const bool inside = s <= w.s_in;                   // step(length(rpos), r) == 1
-        const uint64_t inside_mask = __builtin_amdgcn_ballot_w64(inside);  // scalar tests only
-        if ((inside_mask | (uint64_t)(uint32_t)f.cam_negzero) != 0) {
-          moved |= inside_mask;
-          const float cs = inside ? 1.0f : 0.0f;
-          const float b = cs * 2.0f * ((rx * dx + ry * dy) + rz * dz);
-          const float c = cs * s - w.rr;
-          const float tosurf = cs * (-b + fabsf(sqrt_cr(b * b - 4.0f * c))) * 0.5f;
-          px = px + dx * tosurf;
-          py = py + dy * tosurf;
-          pz = pz + dz * tosurf;
-          total = total + tosurf;
-        }
-        draw = inside ? k : draw;
-      }
+      for (; k < f.sc; k++) wall_visit(k, moved);
       k = 0;
       if (!moved) break;  // uniform: a pass in which no lane moved is a fixed point
     }
@@ -325,7 +395,7 @@ __global__ __launch_bounds__(256) void k_glsl(GlslFrame f) {
   const int r = ty * 8 + (lane >> 3);
   if (i >= f.width || r >= f.rows) return;
   uint32_t work = 0;
-  fragment(f, as_const(f.walls), as_const(f.balls), i, f.row0 + r, work);
+  fragment<false>(f, as_const(f.walls), as_const(f.balls), i, f.row0 + r, work);
 }
 
 // One 8x8 tile per one-wave workgroup in the adaptive tile order (sfrt_device.h
@@ -353,7 +423,7 @@ __global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
   // branch around fragment() would cost its wave-uniform skips their uniformity.
   const bool in = i < f.width && r < f.rows;
   uint32_t work = 0;
-  fragment(f, as_const(f.walls), as_const(f.balls), i < f.width ? i : f.width - 1,
+  fragment<true>(f, as_const(f.walls), as_const(f.balls), i < f.width ? i : f.width - 1,
                   f.row0 + (r < f.rows ? r : f.rows - 1), work, in);
   if (f.tile_cost) {
     const uint32_t w = wave_max_u32(work);  // the tile's longest march

@@ -9,6 +9,7 @@
 //   rt.draw(sp, &world.shader)      Source.cpp:150-153 (one fragment per render-target pixel)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -207,6 +208,19 @@ struct sfrt_glsl {
         if ((rx * rx + ry * ry) + rz * rz <= walls[j].s_in) break;
       }
       f.wall_start = j < sc ? j : 3 * sc;  // inside no wall: no lane ever moves
+    }
+    // The wall cull's margin: every wall-pass position lies inside (or on) some wall reached from
+    // campos, so its coordinates are bounded by R = max(|campos|, max_k |c_k| + r_k); the
+    // positions' binary32 drift over <= 3 sc moves stays below 4e-6 R
+    f.wall_cull_margin = 0.0f;
+    if (!f.cam_negzero && sc > 0 && sc <= 64) {
+      double R = std::max({std::fabs((double)v.campos[0]), std::fabs((double)v.campos[1]),
+                           std::fabs((double)v.campos[2])});
+      for (int k = 0; k < sc; k++)
+        for (int c = 0; c < 3; c++)
+          R = std::max(R, std::fabs((double)v.spheres[k][c]) + std::fabs((double)v.spheres[k][3]));
+      const double m = 1e-3 * R + 1e-4;
+      if (std::isfinite(m) && m < 1e30) f.wall_cull_margin = (float)m;
     }
     if (staged_version == u_version && cur_slot >= 0) {  // launched() re-marks the slot
       HIP_TRY(slots[cur_slot].use_on(s));  // staged, or last read, on another stream: wait for it

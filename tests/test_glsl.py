@@ -172,6 +172,49 @@ def test_gpu_matches_oracle(shader, floor, case):
     assert oracle.fnv1a64(got) == GOLDEN["glsl"][key]["fnv1a64"]
 
 
+def draw_ordered(shader, u, w, h):
+    """The ordered kernel (sfrt_glsl_draw into a device frame: the adaptive tile order and the
+    per-wave wall cull), after a warm-up draw so that the tile order is in use."""
+    import torch
+    shader.set_uniforms(u)
+    b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+    for _ in range(3):
+        shader.draw(b.data_ptr(), w, h, w * 4, 0, h, 0)
+    shader.check(0)
+    return b.cpu().numpy().ravel()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", GLSL_CASES, ids=[c[0] for c in GLSL_CASES])
+def test_gpu_ordered_kernel_matches_oracle(shader, floor, case):
+    """The ordered kernel bench.py times culls each wave's walls to those its rays can meet
+    (glsl_trace.hip wall_mask): the same bytes as the oracle and as the row-major kernel, which
+    visits every wall."""
+    key, w, h, make = case
+    u = make(w, h)
+    got = draw_ordered(shader, u, w, h)
+    assert oracle.fnv1a64(got) == GOLDEN["glsl"][key]["fnv1a64"], key
+    if w * h <= 640 * 360:
+        want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+        assert np.array_equal(got, want), first_diff(got, want, w)
+
+
+@pytest.mark.gpu
+def test_gpu_wall_cull_random_scenes(shader, floor):
+    """The wall cull on 48 random scenes (3-60 walls, random camera and rotation, some with a
+    wide field of view): the ordered kernel's frame equals the oracle's."""
+    rng = np.random.default_rng(5)
+    for seed in range(48):
+        nw, nl, nb = int(rng.integers(3, 61)), int(rng.integers(0, 4)), int(rng.integers(0, 12))
+        w, h = (160, 90) if seed % 3 else (96, 64)
+        u = gs.random_uniforms(100 + seed, nw, nl, nb, w, h)
+        if seed % 4 == 0:
+            u["fov"] = (np.float32(rng.uniform(1.5, 2.6)), np.float32(rng.uniform(1.0, 2.0)))
+        got = draw_ordered(shader, u, w, h)
+        want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+        assert np.array_equal(got, want), (seed, nw, first_diff(got, want, w))
+
+
 @pytest.mark.gpu
 def test_gpu_synthetic_ground_mips(shader, floor):
     """Non-square ground (64x32: 2x1 box levels) over the default uniforms."""
