@@ -97,7 +97,7 @@ __device__ __forceinline__ uint64_t wall_mask(const GlslFrame& f, float dx, floa
              __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dz), 63));
   const float al = __builtin_amdgcn_sqrtf((ax * ax + ay * ay) + az * az);
   if (!(al > 0.5f)) return ~0ull;  // the corner rays more than 120 degrees apart: no cull
-  const float ia = 1.0f / al;
+  const float ia = __builtin_amdgcn_rcpf(al);  // (1 ulp: the margin dwarfs it)
   ax *= ia; ay *= ia; az *= ia;
   // the largest |d x a| over the wave (bit patterns of non-negative floats), and every ray within
   // 60 degrees of the axis (d . a >= 0.5)
@@ -115,9 +115,10 @@ __device__ __forceinline__ uint64_t wall_mask(const GlslFrame& f, float dx, floa
     const float wl = __builtin_amdgcn_sqrtf((wx * wx + wy * wy) + wz * wz);
     const float reach = w.r + f.wall_cull_margin;
     if (wl >= reach) {  // else the camera is within reach of the wall: kept
-      const float ca = ((wx * ax + wy * ay) + wz * az) / wl;                  // cos alpha
+      const float iw = __builtin_amdgcn_rcpf(wl);
+      const float ca = ((wx * ax + wy * ay) + wz * az) * iw;                  // cos alpha
       const float qx = wy * az - wz * ay, qy = wz * ax - wx * az, qz = wx * ay - wy * ax;
-      const float sa = __builtin_amdgcn_sqrtf((qx * qx + qy * qy) + qz * qz) / wl;  // sin alpha
+      const float sa = __builtin_amdgcn_sqrtf((qx * qx + qy * qy) + qz * qz) * iw;  // sin alpha
       const float s_at = sa * cos_t - ca * sin_t;   // sin(alpha - theta)
       const float c_at = ca * cos_t + sa * sin_t;   // cos(alpha - theta)
       const float dist = s_at <= 0.0f ? 0.0f : (c_at <= 0.0f ? wl : wl * s_at);

@@ -63,7 +63,10 @@ struct V3 {
 // when the cell is hit (id = code - kVoxCellBias).
 __device__ __forceinline__ bool cell_hit(const VoxFrame& f, int32_t x, int32_t y, int32_t z,
                                          uint32_t& code) {
-  const uint32_t key = ((uint32_t)x << 20) + ((uint32_t)y << 10) + (uint32_t)z;
+  // ((x << 10) + y) << 10) + z: two v_lshl_add_u32 (left alone: two shifts and an add3)
+  uint32_t key;
+  __asm__("v_lshl_add_u32 %0, %1, 10, %2" : "=v"(key) : "v"(x), "v"(y));
+  __asm__("v_lshl_add_u32 %0, %1, 10, %2" : "=v"(key) : "v"(key), "v"(z));
   const __amdgpu_buffer_rsrc_t cells =
       __builtin_amdgcn_make_buffer_rsrc((void*)f.cells, (short)0, (int)f.cell_bytes, 0x00020000);
   code = __builtin_amdgcn_raw_buffer_load_b8(cells, (int)key, 0, 0);
@@ -268,11 +271,14 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   // branches per step (tools/isa_block_profile.py).  Here a lane tests one stop condition at the
   // bottom of the step, and what stopped it is read from registers afterwards: `early` != 0 (a
   // billboard's texel, alpha > 127), else `hcode` != 0 (the cell code of a block), else it marched
-  // out.  A lane stopped by a billboard still advances in that step; nothing of it but `early` is
-  // read afterwards.  The first loop test is uniform (dist = 0, i = 0).  4K 234.6 -> 208.7 us, and
-  // 208.0 -> 201.5 with the outcome read back this way and colRay kept in the loop (the empty asm
-  // below: sunk past the loop, the axis choice carried two lane masks merged with EXEC every step)
-  // (profiles/ab/r5_ab1, r5_ab2).
+  // out.  A billboard's texel stops its lane through the loop test (the step's distance made
+  // +inf); the lane still advances in that step, and nothing of it but `early` is read afterwards.
+  // The first loop test is uniform (dist = 0, i = 0).  4K 234.6 -> 208.7 us, and 208.0 -> 201.5
+  // with the outcome read back this way and colRay kept in the loop (the empty asm below: sunk
+  // past the loop, the axis choice carried two lane masks merged with EXEC every step)
+  // (profiles/ab/r5_ab1, r5_ab2); with the two-instruction key, the billboard stop through the
+  // distance and the step counters compiled out when no tile cost is recorded (k_voxel_ordered
+  // COST): 200.8 -> 192.3 us (r5_ab4).
   uint32_t hcode = 0u, early = 0u;
   if (0.0f < f.view_distance && 0u < f.maxiter) {
     for (uint32_t i = 0;;) {
@@ -301,7 +307,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       }
       const float rs2 = raySpeed + 0.002f;
       colRay = ax ? 1 : (ay ? 2 : 3);
-      const float tryDist = dist + raySpeed;
+      float tryDist = dist + raySpeed;
       // dynamic billboards in front of the next block (World.cpp:353-378): the next billboard's
       // distance is held in a register (NaN past the last), so the test reads no memory on the
       // steps that pass no billboard (nearly all), and a wave whose lanes all pass none skips
@@ -335,6 +341,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
                 early = pack(to_u8(min255((float)(c & 0xffu) * d.r)),
                              to_u8(min255((float)((c >> 8) & 0xffu) * d.g)),
                              to_u8(min255((float)((c >> 16) & 0xffu) * d.b)), c >> 24);
+                tryDist = __builtin_inff();  // stops the lane through the loop test
                 break;
               }
             }
@@ -351,7 +358,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       __asm__ volatile("; colRay" : "+v"(colRay));  // keeps the axis choice a loop register
       cell_hit(f, pix, piy, piz, hcode);  // hcode != 0: hit a block (World.cpp:385)
       i++;
-      if ((early != 0u) | (hcode != 0u) | !(dist < f.view_distance) | !(i < f.maxiter)) break;
+      if ((hcode != 0u) | !(dist < f.view_distance) | !(i < f.maxiter)) break;
     }
   }
   if (early != 0u) return early;  // a billboard's texel with alpha > 127: never 0
@@ -381,6 +388,9 @@ __device__ uint32_t raycast(const VoxFrame& f, V3 dir, float yscale,
 #ifndef SFRT_VOX_WAVES
 #define SFRT_VOX_WAVES 8
 #endif
+// COST: record the tile's cost for the adaptive order (f.tile_cost set); without it the step
+// counters are dead code and compiled out (one VALU per DDA and shadow-ray step)
+template <bool COST>
 __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f, int tiles_x, int ntiles) {
   const int lane = threadIdx.x & 63;
   int slot = (int)blockIdx.x;
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f
   const int lane2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const int a2 = tx * 8 + (lane2 & 7), r2 = ty * 8 + (lane2 >> 3);
   if (a2 < f.sub_w && r2 < f.sub_rows) f.out[(long long)r2 * f.out_pitch + a2] = rgba;
-  if (f.tile_cost) {
+  if (COST) {
     // the tile's slowest ray, in DDA + shadow steps / 4 (the classes' scale)
     const uint32_t w = wave_max_u32(work);
     if (lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket(w >> 2);
@@ -440,8 +450,12 @@ int launch_voxel(const VoxFrame& f, void* stream) {
     return -1;
   if (tiles > 0x7ffffffeLL) return -1;
   // row-major unless the host linked this launch into its tile-order chain
-  hipLaunchKernelGGL(k_voxel_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,
-                     (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
+  if (f.tile_cost)
+    hipLaunchKernelGGL(k_voxel_ordered<true>, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64),
+                       0, (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
+  else
+    hipLaunchKernelGGL(k_voxel_ordered<false>, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64),
+                       0, (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -51,8 +51,9 @@ MAX_BLOCKS = 64 * 12
 KERNELS = {
     "sphere": {"src": "sphere_trace.hip", "obj": "sphere_trace.o",
                "symbol": "_ZN4sfrt12_GLOBAL__N_116k_trace_window_rILi4EEEvNS_10InlineArgsE"},
+    # k_voxel_ordered<false>: the launch without tile costs (the voxel default)
     "voxel": {"src": "voxel_trace.hip", "obj": "voxel_trace.o",
-              "symbol": "_ZN4sfrt12_GLOBAL__N_115k_voxel_orderedENS_8VoxFrameEii"},
+              "symbol": "_ZN4sfrt12_GLOBAL__N_115k_voxel_orderedILb0EEEvNS_8VoxFrameEii"},
     "glsl": {"src": "glsl_trace.hip", "obj": "glsl_trace.o",
              "symbol": "_ZN4sfrt12_GLOBAL__N_114k_glsl_orderedENS_9GlslFrameEi"},
 }
@@ -509,31 +510,43 @@ def regions_glsl(blocks):
         "lighting": "// ---- lighting",
     }.items()}
     lp = Loops(blocks)
-    loops = {k: lp.innermost(loops_with(blocks, "fragment", A[k]))
-             for k in ("wall_loop", "march_loop", "ball_loop", "light_loop", "shadow_loop")}
-    for k, v in loops.items():
-        if len(v) != 1:
-            raise SystemExit(f"glsl loop {k}: {v}")
-    L = {k: next(iter(v)) for k, v in loops.items()}
+
+    def frag_line(ch):
+        """The line of fragment() (or of a lambda inside it) the instruction belongs to."""
+        for fn, f, ln in ch:
+            if f == "glsl_trace.hip" and (fn.startswith("fragment") or fn.startswith("operator()")):
+                return fn, ln
+        return None, None
+
+    def loops_at(line):
+        return lp.innermost({b["header"] for b in blocks for ch in b["chains"]
+                             if b["header"] and frag_line(ch)[1] == line})
+    L = {k: loops_at(A[k]) for k in ("wall_loop", "march_loop", "ball_loop", "light_loop",
+                                      "shadow_loop")}
+    for k, v in L.items():
+        if not v:
+            raise SystemExit(f"glsl loop {k} not found")
 
     def region(b, ch):
         names = [fn for fn, _, _ in ch]
         if any(n.startswith("sort_tiles") for n in names):
             return "sorter"
-        fn, line = frame_of(ch, "fragment")
+        if any(n.startswith("wall_mask") for n in names):
+            return "wall_cull"
+        fn, line = frag_line(ch)
         if b["rare"]:
             return "rare"
         h = b["header"]
         inr = lambda a, z: line is not None and A[a] <= line <= A[z]
-        if lp.inside(h, {L["ball_loop"]}):
+        if lp.inside(h, L["ball_loop"]):
             return "ball_body" if inr("ball_body_first", "ball_body_last") else "ball_test"
-        if lp.inside(h, {L["march_loop"]}):
+        if lp.inside(h, L["march_loop"]):
             return "march_step"
-        if lp.inside(h, {L["wall_loop"]}):
+        if lp.inside(h, L["wall_loop"]):
             return "wall_inside" if inr("wall_inside_first", "wall_inside_last") else "wall_test"
-        if lp.inside(h, {L["shadow_loop"]}):
+        if lp.inside(h, L["shadow_loop"]):
             return "shadow_body" if inr("shadow_body_first", "shadow_body_last") else "shadow_test"
-        if lp.inside(h, {L["light_loop"]}):
+        if lp.inside(h, L["light_loop"]):
             return "light"
         if fn is None or line is None or line < A["texture"]:
             return "setup"
