@@ -453,7 +453,7 @@ def loops_with(blocks, fname, line):
 
 def regions_voxel(blocks):
     A = {k: src_anchor("voxel", v) for k, v in {
-        "main_loop": "const float tryDist = dist + raySpeed;",
+        "main_loop": "float tryDist = dist + raySpeed;",
         "billboard_first": "V3 bp = pos;",
         "billboard_last": "dnext = DI < f.ndyn ? f.dyn[DI].dist : __builtin_nanf(\"\");\n        }",
         "light_loop": "const VoxLight L = light_at(lp, 0);",
@@ -469,7 +469,7 @@ def regions_voxel(blocks):
 
     def region(b, ch):
         names = [fn for fn, _, _ in ch]
-        if b["rare"] or any(n.endswith("<false>") for n in names):
+        if b["rare"] or any(n.startswith(("raycast_t<false>", "lraycast_t<false>")) for n in names):
             return "rare_plain_division"
         if any(n.startswith("sort_tiles") for n in names):
             return "sorter"
