@@ -220,14 +220,54 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
     for (;;) {
       ++steps;
       const float tx = cx + dx * ball_dist, ty = cy + dy * ball_dist, tz = cz + dz * ball_dist;
-      smooth = 999999999.0f;
-      closest = 0;
-      float shortest = 9999999.0f;
-      snx = sny = snz = 0.0f;
-      // Dominance threshold (t*(1+1e-5) + 1e-4)*(1+6e-6), t = max(smooth + 0.5, shortest, 0.5),
-      // rounded up (kThrMul, kThrAdd); it only changes when a ball's body runs.
-      float thr = 1e30f;
-      for (int k = 0; k < nballs; k++) {
+      float shortest, thr;
+      // The step's first ball runs its body for every lane (its dominance test compares with
+      // (r_skip + 1e30)^2 = inf), from the step's start values, where polsmin's h is +0 once
+      // |999999999 - other| >= 0.5: for a wave whose every lane has other <= 999999936 (the float
+      // below 1e9) the body reduces to these assignments, the same bits: no test,
+      // no start values, no polsmin for it (4K 399.2 -> 385.9 us, profiles/ab/r5_ab6).
+      auto body = [&](const GlslBall& b, int k, float ox, float oy, float oz) {
+        const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100
+        const float other = sqrt_cr(ss) - b.r;
+        const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
+        smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
+        closest = other < shortest ? f.sc + k : closest;                  // :105
+        shortest = gmin(shortest, other);
+        const float nf = gclamp(other, 0.0f, 0.5f) * 2.0f;
+        snx = nf * snx - (1.0f - nf) * ox;
+        sny = nf * sny - (1.0f - nf) * oy;
+        snz = nf * snz - (1.0f - nf) * oz;
+        thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
+      };
+      if (nballs > 0) {
+        const GlslBall b = ld(balls, 0);
+        const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
+        const float ss = (ox * ox + oy * oy) + oz * oz;
+        const float other = sqrt_cr(ss) - b.r;
+        if (__builtin_amdgcn_ballot_w64(!(other <= 999999936.0f))) {
+          smooth = 999999999.0f;  // the literal body from the start values
+          closest = 0;
+          shortest = 9999999.0f;
+          snx = sny = snz = 0.0f;
+          body(b, 0, ox, oy, oz);
+        } else {
+          smooth = other;  // gmin(999999999, other) - (+0)
+          closest = other < 9999999.0f ? f.sc : 0;
+          shortest = gmin(9999999.0f, other);
+          const float nf = gclamp(other, 0.0f, 0.5f) * 2.0f;
+          snx = 0.0f - (1.0f - nf) * ox;  // nf * (+0) - ...
+          sny = 0.0f - (1.0f - nf) * oy;
+          snz = 0.0f - (1.0f - nf) * oz;
+          thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
+        }
+      } else {
+        smooth = 999999999.0f;
+        closest = 0;
+        shortest = 9999999.0f;
+        snx = sny = snz = 0.0f;
+        thr = 1e30f;
+      }
+      for (int k = 1; k < nballs; k++) {
         const GlslBall b = ld(balls, k);
         const float ox = b.x - tx, oy = b.y - ty, oz = b.z - tz;
         // Dominated ball: if otherDist >= max(smooth + 0.5, shortest, 0.5) (with
@@ -241,17 +281,7 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
         const float bnd = b.r_skip + thr;
         const bool dominated = ssf >= bnd * bnd;
         if (!__builtin_amdgcn_ballot_w64(!dominated)) continue;
-        const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's length(), :100
-        const float other = sqrt_cr(ss) - b.r;
-        const float h = gmax(0.5f - fabsf(smooth - other), 0.0f) / 0.5f;  // polsmin(:57-61)
-        smooth = gmin(smooth, other) - h * h * 0.5f * (1.0f / 4.0f);
-        closest = other < shortest ? f.sc + k : closest;                  // :105
-        shortest = gmin(shortest, other);
-        const float nf = gclamp(other, 0.0f, 0.5f) * 2.0f;
-        snx = nf * snx - (1.0f - nf) * ox;
-        sny = nf * sny - (1.0f - nf) * oy;
-        snz = nf * snz - (1.0f - nf) * oz;
-        thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;
+        body(b, k, ox, oy, oz);
       }
       ball_dist += smooth + 0.01f;
       if (!((ball_dist < total) & (smooth > 0.01f) & (steps < kGlslMarchCap))) break;

@@ -258,6 +258,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   int DI = 0;
   float dnext = f.ndyn > 0 ? f.dyn[0].dist : __builtin_nanf("");  // next billboard; NaN: never >=
   int colRay = 0;
+  float last_x = 0.0f, last_y = 0.0f, last_z = 0.0f;  // the last step's rays (colRay, below)
   // Shading after the loop: a lane that hits a block (or a billboard's opaque texel) stops
   // stepping, and the wave shades all its hit lanes once, after its last lane has stopped.
   // Shaded inside the loop, the light loop and its shadow rays ran once per distinct hit step
@@ -274,11 +275,13 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
   // out.  A billboard's texel stops its lane through the loop test (the step's distance made
   // +inf); the lane still advances in that step, and nothing of it but `early` is read afterwards.
   // The first loop test is uniform (dist = 0, i = 0).  4K 234.6 -> 208.7 us, and 208.0 -> 201.5
-  // with the outcome read back this way and colRay kept in the loop (the empty asm below: sunk
-  // past the loop, the axis choice carried two lane masks merged with EXEC every step)
+  // with the outcome read back this way and the axis choice kept out of the loop's lane masks
   // (profiles/ab/r5_ab1, r5_ab2); with the two-instruction key, the billboard stop through the
   // distance and the step counters compiled out when no tile cost is recorded (k_voxel_ordered
-  // COST): 200.8 -> 192.3 us (r5_ab4).
+  // COST): 200.8 -> 192.3 us (r5_ab4).  The hit face's axis (colRay) is recomputed after the loop
+  // from the lane's last step's rays, by the step's own rule: computed in the loop it cost two
+  // selects per step, and left for the compiler to sink it carried two lane masks merged with
+  // EXEC every step (193.3 -> 188.0 us, r5_ab6).
   uint32_t hcode = 0u, early = 0u;
   if (0.0f < f.view_distance && 0u < f.maxiter) {
     for (uint32_t i = 0;;) {
@@ -306,7 +309,7 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
         raySpeed = ax ? xray : (ay ? yray : zray);
       }
       const float rs2 = raySpeed + 0.002f;
-      colRay = ax ? 1 : (ay ? 2 : 3);
+      last_x = xray; last_y = yray; last_z = zray;
       float tryDist = dist + raySpeed;
       // dynamic billboards in front of the next block (World.cpp:353-378): the next billboard's
       // distance is held in a register (NaN past the last), so the test reads no memory on the
@@ -355,13 +358,22 @@ __device__ uint32_t raycast_t(const VoxFrame& f, V3 dir, float yscale,
       pos.y += dir.y * (ay ? rs2 : raySpeed);
       pos.z += dir.z * ((ax | ay) ? raySpeed : rs2);
       pix = pos_i32<RECIP>(pos.x); piy = pos_i32<RECIP>(pos.y); piz = pos_i32<RECIP>(pos.z);
-      __asm__ volatile("; colRay" : "+v"(colRay));  // keeps the axis choice a loop register
       cell_hit(f, pix, piy, piz, hcode);  // hcode != 0: hit a block (World.cpp:385)
       i++;
       if ((hcode != 0u) | !(dist < f.view_distance) | !(i < f.maxiter)) break;
     }
   }
   if (early != 0u) return early;  // a billboard's texel with alpha > 127: never 0
+  // the axis of the lane's last step, from that step's rays (kept in registers: the loop's last
+  // assignment is its exit value), by the step's own rule
+  if (RECIP) {
+    const float rs = fminf(fminf(last_x, last_y), last_z);
+    colRay = last_x == rs ? 1 : (last_y == rs ? 2 : 3);
+  } else {
+    const bool ax = (last_x <= last_y) & (last_x <= last_z);
+    const bool ay = !ax & (last_y <= last_x) & (last_y <= last_z);
+    colRay = ax ? 1 : (ay ? 2 : 3);
+  }
   if (hcode != 0u)
     return shade_hit<RECIP>(f, pos, pix, piy, piz, colRay, sx, sy, sz, dist,
                             (int)hcode - kVoxCellBias, work);

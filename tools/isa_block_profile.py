@@ -500,8 +500,10 @@ def regions_glsl(blocks):
         "wall_inside_last": "total = total + tosurf;",
         "march_loop": "ball_dist += smooth + 0.01f;",
         "ball_loop": "const bool dominated = ssf >= bnd * bnd;",
-        "ball_body_first": "const float ss = (ox * ox + oy * oy) + oz * oz;",
-        "ball_body_last": "thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul",
+        "ball_body_first": "const float ss = (ox * ox + oy * oy) + oz * oz;  // the shader's",
+        "ball_body_last": "thr = fmaxf(fmaxf(smooth + 0.5f, shortest), 0.5f) * kThrMul + kThrAdd;\n      };",
+        "ball_first_first": "if (nballs > 0) {",
+        "ball_first_last": "thr = 1e30f;",
         "light_loop": "const float tlx = L.x - px, tly = L.y - py, tlz = L.z - pz;",
         "shadow_loop": "const float cosang = (-tnx * P.ux + -tny * P.uy) + -tnz * P.uz;",
         "shadow_body_first": "float sangle = sfrt_math::acosf(cosang);",
@@ -541,6 +543,9 @@ def regions_glsl(blocks):
         if lp.inside(h, L["ball_loop"]):
             return "ball_body" if inr("ball_body_first", "ball_body_last") else "ball_test"
         if lp.inside(h, L["march_loop"]):
+            # the step's first ball (specialized, or the lambda's body inlined for it)
+            if inr("ball_first_first", "ball_first_last") or inr("ball_body_first", "ball_body_last"):
+                return "ball_first"
             return "march_step"
         if lp.inside(h, L["wall_loop"]):
             return "wall_inside" if inr("wall_inside_first", "wall_inside_last") else "wall_test"
