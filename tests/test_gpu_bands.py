@@ -568,3 +568,80 @@ def test_row_costs_invalid_after_unordered_fill(floor_tex):
     assert (r0, c.size) == (200, 400)
     w.check()
     w.close()
+
+
+def _nccl_one_rank_worker(port, key, out_path):
+    """bench.py's N > 1 calls on the real RCCL backend, at the one world size a one-GPU box
+    allows: init_process_group("nccl", device_id=...) with a timeout, the band rendered on a
+    dedicated stream and gathered by dist.gather(async_op=True) into rank 0's frame view on
+    that stream (BandPipeline.submit's equal-band call), max_over_ranks as an all_reduce of a
+    device tensor, the gloo host group and barriers beside it."""
+    import sys
+    for p in (os.path.join(ROOT, "sfml-software-raytracer_amd"), os.path.join(ROOT, "oracle"), ROOT):
+        sys.path.insert(0, p)
+    from datetime import timedelta
+    import torch
+    import torch.distributed as dist
+    import bands
+    import oracle
+    import scenes as sc
+    import sfrt
+    res = {"stage": "init"}
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, device_id=torch.device("cuda", 0),
+                                timeout=timedelta(seconds=60))
+        host = dist.new_group(backend="gloo", timeout=timedelta(seconds=60))
+        res["backend"] = dist.get_backend()
+        g = GOLDEN["frames"][key]
+        width, height = g["width"], g["height"]
+        pitch = width * 4
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
+        w = sfrt.World(0)
+        w.load_texture(*sc.load_floor())
+        w.set_scene(sc.SCENES[g["scene"]]().posed(*g["pose"]), width, height)
+        frames = [torch.full((height, pitch), 0xA5, dtype=torch.uint8, device="cuda:0")
+                  for _ in range(2)]
+        band = torch.empty(height, pitch, dtype=torch.uint8, device="cuda:0")
+        hashes = []
+        res["stage"] = "gather"
+        for k in range(4):  # two slots, each reused: the gather orders after the render
+            w.render_band(band.data_ptr(), pitch, 0, height, stream.cuda_stream)
+            work = dist.gather(band, [frames[k % 2]], dst=0, async_op=True)
+            work.wait()
+            hashes.append(oracle.fnv1a64(frames[k % 2].cpu().numpy()))
+        w.check(stream.cuda_stream)
+        w.close()
+        res["stage"] = "reduce"
+        res["max"] = bands.max_over_ranks(1.25, device="cuda:0")
+        dist.barrier(group=host)
+        dist.barrier()
+        res.update(stage="done", ok=all(h == g["fnv1a64"] for h in hashes))
+        dist.destroy_process_group()
+    except Exception as e:  # reported to the test, which fails with it
+        res["error"] = repr(e)
+    with open(out_path, "w") as fh:
+        json.dump(res, fh)
+
+
+def test_torch_distributed_nccl_one_rank(tmp_path):
+    """The RCCL backend of torch.distributed on the device (bench.py:773's init, BandPipeline's
+    gather of device bands, max_over_ranks on a device tensor): one rank, as the one-GPU box
+    allows -- RCCL refuses two ranks on one device, so N > 1 runs only on the driver's node.
+    The gathered frames hash to the golden value."""
+    import multiprocessing
+    out = str(tmp_path / "res.json")
+    ctx = multiprocessing.get_context("spawn")
+    p = ctx.Process(target=_nccl_one_rank_worker,
+                    args=(_free_port(), "c2_1920x1080_default10@0,0", out))
+    p.start()
+    p.join(150)
+    if p.is_alive():
+        p.kill()
+        p.join()
+        pytest.fail("the RCCL one-rank process did not finish in 150 s")
+    res = json.load(open(out))
+    assert res.get("stage") == "done" and res.get("ok"), res
+    assert res["backend"] == "nccl" and res["max"] == 1.25, res
