@@ -181,6 +181,54 @@ def default_world(cam_pos=(15.5, 1.9, 15.5), rotation=0.0, hrotation=0.0) -> Vox
                       float(rotation), float(hrotation))
 
 
+def random_world(seed: int) -> tuple[VoxelScene, int, int]:
+    """Stress snapshot (tests only): a random block grid of random size (textures 0-3 and colours
+    -1..-5, some with floor and border walls), the camera in an empty cell with random turn and
+    tilt, 0-10 billboards near it in list order by distance, 0-12 lights with and without
+    shadows, random view and shadow distances.  Returns (scene, width, height)."""
+    rng = np.random.default_rng(seed)
+    nx, ny, nz = int(rng.integers(8, 49)), int(rng.integers(4, 13)), int(rng.integers(8, 49))
+    b = np.full((nx, ny, nz), EMPTY, dtype=np.int16)
+    ids = np.array([0, 1, 2, 3, -1, -2, -3, -4, -5], dtype=np.int16)
+    fill = rng.random(b.shape) < rng.uniform(0.02, 0.15)
+    b[fill] = rng.choice(ids, size=int(fill.sum()))
+    if rng.random() < 0.7:
+        b[:, 0, :] = rng.choice(ids)
+    if rng.random() < 0.5:
+        wall = rng.choice(ids)
+        b[0, :, :] = b[-1, :, :] = b[:, :, 0] = b[:, :, -1] = wall
+    while True:  # the camera in an empty interior cell
+        c = (int(rng.integers(1, nx - 1)), int(rng.integers(1, ny - 1)), int(rng.integers(1, nz - 1)))
+        if b[c] == EMPTY:
+            break
+    cam = np.array([F(c[k] + rng.uniform(0.05, 0.95)) for k in range(3)], F)
+    rotation, hrotation = F(rng.uniform(0, 2 * np.pi)), F(rng.uniform(-0.6, 0.6))
+    dyn = np.zeros(int(rng.integers(0, 11)), dtype=DYN_DTYPE)
+    for d in dyn:
+        off = rng.uniform(1.0, 8.0) * np.array([np.sin(a := rng.uniform(0, 2 * np.pi)), 0, np.cos(a)])
+        pos = np.array([cam[0] + off[0], rng.uniform(0.3, ny - 0.7), cam[2] + off[2]], F)
+        to = pos - cam
+        d["pos"], d["size"] = pos, (rng.uniform(0.05, 0.5), rng.uniform(0.1, 0.8))
+        d["r"], d["g"], d["b"] = rng.uniform(0, 2, 3).astype(F)
+        d["dist_to_camera"] = sqrtf(F(F(to[0] * to[0]) + F(to[2] * to[2])))
+        d["texture_id"] = int(rng.integers(0, 2))
+    dyn = dyn[np.argsort(dyn["dist_to_camera"], kind="stable")]
+    lights = np.zeros(int(rng.integers(0, 13)), dtype=LIGHT_DTYPE)
+    for L in lights:
+        if rng.random() < 0.5:  # near the camera
+            L["pos"] = np.clip(cam + rng.uniform(-6, 6, 3).astype(F), 0.2, [nx - 0.2, ny - 0.2, nz - 0.2])
+        else:
+            L["pos"] = (rng.uniform(0, nx), rng.uniform(0.2, ny - 0.2), rng.uniform(0, nz))
+        L["intensity"] = rng.uniform(1.0, 12.0)
+        L["r"], L["g"], L["b"] = rng.uniform(0.2, 1.0, 3).astype(F)
+        L["shadows"] = int(rng.random() < 0.6)
+    scene = VoxelScene(b, dyn, lights, tuple(float(v) for v in cam), float(rotation),
+                       float(hrotation), shadow_distance=float(rng.choice([8.0, 16.0])),
+                       view_distance=float(rng.choice([12.0, 24.0, 40.0])))
+    w, h = [(320, 180), (256, 144), (333, 187)][seed % 3]
+    return scene, w, h
+
+
 def load_textures():
     """textures[0..3] and dynTextures[0..1] (World.cpp:40-45), decoded RGBA8."""
     names = ["Wall", "Floor", "Ceiling", "Block"]
