@@ -646,7 +646,10 @@ def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
             stop_child()
             break
         time.sleep(0.2)
-    rc = child.wait()
+    try:
+        rc = child.wait(timeout=30)
+    except subprocess.TimeoutExpired:  # not gone even after SIGKILL (stuck in the driver): report
+        rc = -9
     for t in threads:
         t.join(timeout=5)
     if rank != 0:
