@@ -1,8 +1,8 @@
 """Build-flag A/B of libsfrt.so builds, interleaved across processes, bytes checked.
 
     python tools/ab_libs.py --libs a.so,b.so,a.so@3 [--rounds 3] [--reps 40] [--cases 4k,4k_rot,...]
-(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE; lib^O sets SFRT_OPT_TILE_ORDER=O on the
-GLSL and voxel renderers; lib#K sets SFRT_AB_KNOB=K for an
+(lib@R forces R pixels per lane, SFRT_OPT_RAYS_PER_LANE; lib^O sets SFRT_OPT_TILE_ORDER=O on every
+renderer; lib#K sets SFRT_AB_KNOB=K for an
 experimental build that reads it -- r2_ab28 read it as SFRT_SPLIT; the product reads none)
 
 Each round starts one process per library (SFRT_LIB=<lib>, the same sfrt.py), which
@@ -105,6 +105,8 @@ def child(cases, reps, rays):
         sc = None
         if w is None:
             w = sphere_world
+            if os.environ.get("SFRT_AB_TILE_ORDER") is not None:  # "lib^O" on the sphere world too
+                w.set_option(sfrt.SFRT_OPT_TILE_ORDER, int(os.environ["SFRT_AB_TILE_ORDER"]))
             sc = scenes.SCENES[sname]().posed(*pose)
             w.set_scene(sc, width, height)
         cam_pos = sc.cam_pos if sc is not None else None
