@@ -411,3 +411,19 @@ def test_voxel_gpu_random_worlds(vworld, assets):
         lit += scene.lights.shape[0] > 0
         billboards += scene.dyn.shape[0] > 0
     assert lit >= 12 and billboards >= 12
+
+
+def test_random_worlds_oracle_deterministic(assets):
+    """The random worlds of test_voxel_gpu_random_worlds on the CPU: the generator is
+    deterministic, the restatement renders them the same with 1 and 8 threads, and none of
+    them makes the reference read outside a texture (so the GPU test's frames are defined)."""
+    for seed in (0, 5, 11, 17, 23):
+        scene, w, h = vs.random_world(seed)
+        again, w2, h2 = vs.random_world(seed)
+        assert (w, h) == (w2, h2) and np.array_equal(scene.blocks, again.blocks)
+        assert np.array_equal(scene.dyn, again.dyn) and np.array_equal(scene.lights, again.lights)
+        o = oracle.VoxelOracle(scene, w, h, assets[0], assets[1], vs.COLORS)
+        before = oracle.VoxelOracle.bad_texel_reads()
+        a = o.render(8)
+        assert oracle.VoxelOracle.bad_texel_reads() == before, seed
+        assert np.array_equal(a, o.render(1)), seed
