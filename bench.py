@@ -576,6 +576,20 @@ def _partial_write(path, result) -> None:
     os.replace(tmp, path)
 
 
+PARTIAL_EXIT = 4  # supervise(): the line carries a measured headline but is incomplete
+
+
+def _die_with_parent() -> None:
+    """preexec_fn of the supervised child (runs in the child before exec; the supervisor has not
+    touched the GPU): SIGKILL when the supervisor exits, whatever ends it."""
+    import ctypes
+    import signal
+    try:
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):
+        pass
+
+
 def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
     """N > 1 (one process per GPU under torch.distributed.run): this rank's body runs in a child
     process (bench.py --worker), so that an RCCL failure -- communicator init, a collective on
@@ -587,8 +601,13 @@ def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
     signalled (torch.distributed.run ends every rank when one rank fails), rank 0 prints the line
     the child had reached (--partial-out: the headline once measured, then every also line) with
     "error" = {stage, exit, detail}, or a line with "value": null when the headline was not
-    reached.  Exit status: 0 when the printed line carries a measured headline, else 1; ranks != 0
-    pass their child's status on.  Reference caller: Source.cpp:47-52."""
+    reached.  Exit status (rank 0): 0 for a complete line, 3 for a complete line with a frame that
+    differs, PARTIAL_EXIT (4) for a line with a measured headline and "complete": false -- so a
+    partial run shows in the status the driver sees, not only in the JSON body -- and 1 for a line
+    with no headline; ranks != 0 pass their child's status on.  The signal handlers it installs are
+    restored before it returns, and the child is killed if the supervisor dies first
+    (PR_SET_PDEATHSIG: the child runs in its own session, out of reach of the group signals
+    torch.distributed.run sends).  Reference caller: Source.cpp:47-52."""
     import collections
     import signal
     import subprocess
@@ -603,7 +622,7 @@ def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
     if partial:
         cmd += ["--partial-out", partial]
     child = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                             start_new_session=True)
+                             start_new_session=True, preexec_fn=_die_with_parent)
     seen = {"line": False}
     tail = collections.deque(maxlen=12)
 
@@ -636,22 +655,25 @@ def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
     def on_signal(signum, _frame):
         why["signal"] = signal.Signals(signum).name
         stop_child()
-    for sg in (signal.SIGTERM, signal.SIGINT):
-        signal.signal(sg, on_signal)
-    deadline = time.monotonic() + time_limit
-    timed_out = False
-    while child.poll() is None:
-        if time.monotonic() > deadline:
-            timed_out = True
-            stop_child()
-            break
-        time.sleep(0.2)
+    previous = {sg: signal.signal(sg, on_signal) for sg in (signal.SIGTERM, signal.SIGINT)}
     try:
-        rc = child.wait(timeout=30)
-    except subprocess.TimeoutExpired:  # not gone even after SIGKILL (stuck in the driver): report
-        rc = -9
-    for t in threads:
-        t.join(timeout=5)
+        deadline = time.monotonic() + time_limit
+        timed_out = False
+        while child.poll() is None:
+            if time.monotonic() > deadline:
+                timed_out = True
+                stop_child()
+                break
+            time.sleep(0.2)
+        try:
+            rc = child.wait(timeout=30)
+        except subprocess.TimeoutExpired:  # not gone even after SIGKILL (stuck in the driver)
+            rc = -9
+        for t in threads:
+            t.join(timeout=5)
+    finally:
+        for sg, h in previous.items():
+            signal.signal(sg, h)
     if rank != 0:
         return rc if rc >= 0 else 1
     line = None
@@ -682,7 +704,7 @@ def supervise(argv, rank: int, world_size: int, time_limit: float) -> int:
                      "exit": rc, "detail": list(tail)[-6:]}
     line["complete"] = False
     print(json.dumps(line), flush=True)
-    return 0 if headline else 1
+    return PARTIAL_EXIT if headline else 1
 
 
 def injected_failure(args, rank: int, world_size: int, where: str) -> None:

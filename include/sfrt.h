@@ -331,7 +331,11 @@ SFRT_API int sfrt_voxel_set_view(sfrt_voxel* v, float shadow_distance, float vie
  * Block::textureID (>= 0: textures[id]; < 0: colors[-id]) or SFRT_VOXEL_EMPTY;
  * lookups keep the map's (x<<20)+(y<<10)+z key semantics.  1 <= nx <= 2048, 1 <= ny, nz
  * <= 1024; the device copy is the key space itself, nx MiB of bytes (100 MiB for a
- * 100-wide world), rewritten by the first frame after each call. */
+ * 100-wide world; 2 GiB for nx = 2048 whatever ny and nz are), rewritten by the first
+ * frame after each call, stream-ordered on that frame's stream (no device-wide sync: it
+ * waits on the device for the launches that read the old grid).  The call itself touches
+ * no device memory: a grid the device cannot allocate fails that first frame call with
+ * SFRT_E_HIP. */
 SFRT_API int sfrt_voxel_set_blocks(sfrt_voxel* v, const int16_t* texture_ids, int nx, int ny, int nz);
 SFRT_API int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h);
 SFRT_API int sfrt_voxel_load_dyn_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h);

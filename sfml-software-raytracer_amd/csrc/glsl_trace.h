@@ -74,6 +74,9 @@ struct GlslFrame {
   uint8_t* tile_cost;
   const uint8_t* prev_cost;
   uint32_t* next_order;
+  // tile_order's classes are the ones in tile_cost: store only changed classes (sfrt_device.h
+  // store_cost, sfrt_sched.h TileSchedPtrs::cost_diff)
+  int32_t cost_diff;
 };
 
 // Tile grid of the ordered GLSL kernel for f: key (> 0) and tile count.

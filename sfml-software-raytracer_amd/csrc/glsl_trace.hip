@@ -86,7 +86,8 @@ constexpr float kThrMul = 0x1.00010ep+0f, kThrAdd = 0x1.a36ed4p-14f;
 // (alpha the angle of w = c - campos from the axis), |w| when alpha - theta >= 90 degrees (the
 // apex is nearest), 0 inside the cone.  A wave whose rays spread past 60 degrees keeps all walls.
 // margin = f.wall_cull_margin (host: 1e-3 of the largest coordinate the pass can reach, + 1e-4),
-// far above the positions' drift (< 4e-6 of it) and this test's own rounding.
+// far above the positions' drift (at most 3 sc moves, each an add and a multiply rounding within
+// 2^-24 of it: 2 * 3 * sc * 2^-24 < 2.3e-5 of it for sc <= 64) and this test's own rounding.
 __device__ __forceinline__ uint64_t wall_mask(const GlslFrame& f, float dx, float dy, float dz) {
   const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   float ax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dx), 0)) +
@@ -442,11 +443,8 @@ __global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
     }
     slot -= 1;
   }
-  int tile = slot;
-  if (f.tile_order) {
-    const int t = (int)f.tile_order[slot];
-    tile = t < ntiles ? t : slot;  // never outside the grid
-  }
+  uint32_t cls;  // the tile's class in the order (sfrt_device.h slot_tile)
+  const int tile = slot_tile(f.tile_order, slot, ntiles, cls);
   const int tx = tile % f.tiles_x, ty = tile / f.tiles_x;
   const int i = tx * 8 + (lane & 7);
   const int r = ty * 8 + (lane >> 3);
@@ -458,7 +456,7 @@ __global__ __launch_bounds__(64) void k_glsl_ordered(GlslFrame f, int ntiles) {
                   f.row0 + (r < f.rows ? r : f.rows - 1), work, in);
   if (f.tile_cost) {
     const uint32_t w = wave_max_u32(work);  // the tile's longest march
-    if (lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket(w);
+    if (lane == 0) store_cost(f.tile_cost, tile, tile_bucket(w), cls, f.cost_diff);
   }
 }
 

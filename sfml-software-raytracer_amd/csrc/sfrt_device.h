@@ -244,8 +244,49 @@ __device__ __forceinline__ uint32_t tile_bucket(uint32_t steps) {
   return (uint32_t)(kTileBuckets - 1) - c;
 }
 
+// Where the order array keeps the tile of dispatch slot `slot` (0 = longest) of an n-tile launch.
+// Slot s runs in workgroup s + 1 (workgroup 0 is the sorter), and workgroups are dealt to the 8
+// XCDs round-robin (observed placement): the entries of the slots one XCD runs are
+// stored together, so each XCD's L2 fetches only its eighth of the array.  Row-major storage had
+// every XCD fetch every line of it -- at 4K 8 x 518 KB for the GLSL kernel's 129,600 tiles, 4.1 MB of
+// the launch's reads.  A bijection of [0, n) into [0, n + 8) (sfrt_sched.h
+// order_capacity).
+__device__ __forceinline__ uint32_t order_index(int slot, int n) {
+  const uint32_t d = (uint32_t)slot + 1u;
+  const uint32_t per = ((uint32_t)n >> 3) + 1u;  // >= ceil((n + 1) / 8)
+  return (d & 7u) * per + (d >> 3);
+}
+
+// An order entry: the tile in the low kOrderTileBits bits and, above them, the tile's class in
+// the cost buffer the order was sorted from (its own, undilated).  That buffer is the one the
+// launch reading the order records into (sfrt_sched.h), so a wave whose class is unchanged need
+// not store it again (TileSchedPtrs::cost_diff): with a still camera no launch stores any.  The
+// cost stores are one byte per tile from every XCD, so each XCD's L2 wrote back a partial copy of
+// the whole array -- at 4K ~1 MB of the GLSL launch's writes.  Chains take grids of
+// fewer than 2^28 tiles (sfrt_sched.h kOrderMaxTiles).
+constexpr int kOrderTileBits = 28;
+constexpr uint32_t kOrderTileMask = (1u << kOrderTileBits) - 1u;
+static_assert(kTileBuckets <= (1 << (32 - kOrderTileBits)), "a class fits above the tile");
+
+// The tile of dispatch slot `slot` of an n-tile launch and the class its order entry carries
+// (kTileBuckets when there is none: row-major launches, a corrupt entry).
+__device__ __forceinline__ int slot_tile(const uint32_t* order, int slot, int n, uint32_t& cls) {
+  cls = (uint32_t)kTileBuckets;
+  if (!order) return slot;
+  const uint32_t e = order[order_index(slot, n)];
+  const int t = (int)(e & kOrderTileMask);
+  if (t >= n) return slot;  // never outside the grid
+  cls = e >> kOrderTileBits;
+  return t;
+}
+
+// Records tile `tile`'s class c, unless diff is set and the order entry already had it (cls).
+__device__ __forceinline__ void store_cost(uint8_t* cost, int tile, uint32_t c, uint32_t cls, int diff) {
+  if (!diff || c != cls) cost[tile] = (uint8_t)c;
+}
+
 // Stable counting sort of n tiles by bucket (longest first; ties in tile
-// order), by one wave.  Each lane owns one contiguous chunk of tiles, read 16
+// order), by one wave, into the slot layout of order_index.  Each lane owns one contiguous chunk of tiles, read 16
 // buckets per 16-byte load with eight loads in flight (the passes are bound by
 // load latency), and its own column of a [bucket][lane] histogram in LDS, so
 // counting and ranking need no atomics; the exclusive scan runs bucket-major
@@ -286,7 +327,10 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
         const uint32_t w[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
         if (!dilate) {
 #pragma unroll
-          for (int e = 0; e < 16; e++) one((w[e >> 2] >> (8 * (e & 3))) & 0xffu, (v + u) * 16 + e);
+          for (int e = 0; e < 16; e++) {
+            const uint32_t c = (w[e >> 2] >> (8 * (e & 3))) & 0xffu;
+            one(c, (v + u) * 16 + e, c);
+          }
           continue;
         }
         const uint32_t nxt = u + 1 < D && v + u + 1 < v1 ? (q[u + 1].x & 0xffu) : after;
@@ -296,7 +340,7 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
           const uint32_t right = e < 15 ? (w[(e + 1) >> 2] >> (8 * ((e + 1) & 3))) & 0xffu : nxt;
           uint32_t m = prev < cur ? prev : cur;  // bucket 0 = longest: the minimum
           m = right < m ? right : m;
-          one(m, (v + u) * 16 + e);
+          one(m, (v + u) * 16 + e, cur);
           prev = cur;
           cur = right;
         }
@@ -304,18 +348,19 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
     }
     if (tail)
       for (int t = nvec * 16; t < n; t++) {
-        uint32_t m = at(t);
+        const uint32_t c = at(t);
+        uint32_t m = c;
         if (dilate) {
           const uint32_t l = at(t - 1), r = at(t + 1);
           m = l < m ? l : m;
           m = r < m ? r : m;
         }
-        one(m, t);
+        one(m, t, c);
       }
   };
   // LDS atomics on the lane's own counters: no conflicts, and the count pass's
   // need no return (a plain read-modify-write would wait on every read)
-  auto count = [&](uint32_t b, int) { atomicAdd(&cnt[b][lane], 1u); };
+  auto count = [&](uint32_t b, int, uint32_t) { atomicAdd(&cnt[b][lane], 1u); };
   if (dilate) pass(std::integral_constant<int, 4>{}, count);
   else pass(std::integral_constant<int, 8>{}, count);
   uint32_t run = 0;  // exclusive scan over (bucket, lane), bucket-major
@@ -331,7 +376,9 @@ __device__ __forceinline__ void sort_tiles(const uint8_t* __restrict__ cost, int
     cnt[b][lane] = run + incl - c;
     run += (uint32_t)__shfl((int)incl, 63, 64);
   }
-  auto place = [&](uint32_t b, int t) { order[atomicAdd(&cnt[b][lane], 1u)] = (uint32_t)t; };
+  auto place = [&](uint32_t b, int t, uint32_t c) {
+    order[order_index((int)atomicAdd(&cnt[b][lane], 1u), n)] = (uint32_t)t | (c << kOrderTileBits);
+  };
   if (dilate) pass(std::integral_constant<int, 4>{}, place);
   else pass(std::integral_constant<int, 8>{}, place);
 }

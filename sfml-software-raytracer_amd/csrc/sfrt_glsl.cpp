@@ -211,7 +211,9 @@ struct sfrt_glsl {
     }
     // The wall cull's margin: every wall-pass position lies inside (or on) some wall reached from
     // campos, so its coordinates are bounded by R = max(|campos|, max_k |c_k| + r_k); the
-    // positions' binary32 drift over <= 3 sc moves stays below 4e-6 R
+    // positions' binary32 drift over <= 3 sc moves (an add and a multiply each, each rounding
+    // within 2^-24 R) stays below 2 * 3 * sc * 2^-24 R < 2.3e-5 R for sc <= 64
+    static_assert(2.0 * 3.0 * 64.0 * 0x1.0p-24 < 1e-3 / 8, "the margin dwarfs the drift");
     f.wall_cull_margin = 0.0f;
     if (!f.cam_negzero && sc > 0 && sc <= 64) {
       double R = std::max({std::fabs((double)v.campos[0]), std::fabs((double)v.campos[1]),
@@ -477,6 +479,7 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
   f.tile_cost = p.tile_cost;
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
+  f.cost_diff = p.cost_diff ? 1 : 0;
   const bool queued = sfrt::launch_glsl(f, s) == 0;
   HIP_TRY(g->sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;

@@ -18,11 +18,21 @@
 
 namespace sfrt {
 
+// Entries of an n-tile order array: its slot layout (sfrt_device.h order_index) maps the n slots
+// into [0, n + 8).
+inline long long order_capacity(long long n) { return n + 8; }
+// Order entries keep the tile in 28 bits (sfrt_device.h kOrderTileBits): larger grids render
+// row-major.
+constexpr long long kOrderMaxTiles = 1ll << 28;
+
 struct TileSchedPtrs {
   const uint32_t* tile_order = nullptr;  // slot -> tile (nullptr: row-major)
   uint8_t* tile_cost = nullptr;          // this launch's per-tile classes (nullptr: no chain)
   const uint8_t* prev_cost = nullptr;    // launch k-1's, to sort (nullptr: no sorter workgroup)
   uint32_t* next_order = nullptr;        // the sorter's output, for launch k+1
+  // tile_order's entries carry the classes now in tile_cost (the buffer they were sorted from,
+  // untouched since): the launch stores only the classes that changed
+  bool cost_diff = false;
 };
 
 struct TileSched {
@@ -38,6 +48,7 @@ struct TileSched {
   hipStream_t last_stream = nullptr;
   bool have_last = false;
   uint64_t used = 0;             // TileChains: when the chain last took a launch
+  bool probed = false;           // a timing-probe launch rewrote cost[k % 2] since k last moved
 
   void release() {
     for (int q = 0; q < 2; q++) {
@@ -56,14 +67,15 @@ struct TileSched {
   hipError_t begin(long long key, long long tiles, hipStream_t s, int mode, TileSchedPtrs& p) {
     p = TileSchedPtrs{};
     pending_key = 0;
-    if (key == 0 || mode == 0) return hipSuccess;
+    if (key == 0 || mode == 0 || tiles >= kOrderMaxTiles) return hipSuccess;
     hipError_t e;
     if (tiles > cap) {  // (re)allocate; a new chain starts
       if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
       release();
       reset();
       for (int q = 0; q < 2; q++) {
-        if ((e = hipMalloc(&order[q], sizeof(uint32_t) * (size_t)tiles)) != hipSuccess) return e;
+        if ((e = hipMalloc(&order[q], sizeof(uint32_t) * (size_t)order_capacity(tiles))) != hipSuccess)
+          return e;
         if ((e = hipMalloc(&cost[q], (size_t)tiles)) != hipSuccess) return e;
       }
       cap = tiles;
@@ -80,8 +92,10 @@ struct TileSched {
     p.next_order = order[(k + 1) & 1];
     if (mode == 2 && sorted_prev && same) {
       p.prev_cost = nullptr;
+      probed = true;  // it stores every class: cost[k % 2] no longer matches order[k % 2]
       return hipSuccess;  // nothing to commit
     }
+    p.cost_diff = p.tile_order != nullptr && !probed;
     pending_key = key;
     pending_sorted = same;
     return hipSuccess;
@@ -103,6 +117,7 @@ struct TileSched {
       key_prev = pending_key;
       k++;
       pending_key = 0;
+      probed = false;
     }
     last_stream = s;
     have_last = true;
@@ -114,6 +129,7 @@ struct TileSched {
     key_prev = 0;
     sorted_prev = false;
     pending_key = 0;
+    probed = false;
   }
 };
 

@@ -71,6 +71,9 @@ struct FrameRec {
   // The camera moved since the launch whose classes the sorter ranks: rank each
   // tile by the longest of it and its row neighbours (sfrt_device.h sort_tiles).
   int order_dilate;
+  // tile_order's classes are the ones in tile_cost: store only changed classes (sfrt_device.h
+  // store_cost, sfrt_sched.h TileSchedPtrs::cost_diff)
+  int32_t cost_diff;
 };
 
 // Kernel argument for n <= kInlineSpheres: frame + spheres in the kernarg segment.

@@ -128,7 +128,17 @@ struct sfrt_voxel {
   DevTex tex[sfrt::kVoxSlots], dyn_tex[sfrt::kVoxSlots];
   uint8_t* d_cells = nullptr;  // the key-indexed byte grid (voxel_trace.h, cell_hit)
   size_t d_cells_cap = 0;
+  // Every byte of d_cells outside planes x < box[0], rows y < box[1], columns z < box[2] is 0.
+  int box[3] = {0, 0, 0};
   bool blocks_dirty = true;
+  // The codes of the last set_blocks on their way to the grid: pinned staging, its device copy,
+  // and the event after the last rewrite that read them (the next upload reuses both).
+  uint8_t* h_codes = nullptr;
+  uint8_t* d_codes = nullptr;
+  size_t codes_cap = 0;
+  hipEvent_t codes_ev = nullptr;
+  bool codes_pending = false;
+  sfrt::SharedBuffer grid;   // the launches reading d_cells, on every stream (sfrt_host.h)
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
   // launches on different streams never see a table overwritten under them.
@@ -159,6 +169,10 @@ struct sfrt_voxel {
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
     (void)hipFree(d_cells);
+    (void)hipFree(d_codes);
+    (void)hipHostFree(h_codes);
+    if (codes_ev) (void)hipEventDestroy(codes_ev);
+    grid.release();
     for (auto& t : slots) t.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
@@ -184,8 +198,9 @@ struct sfrt_voxel {
     const float hIncreaseBy = cam.fov_h / width;
     if (staged_version == tables_version && cur_slot >= 0) {
       sfrt::TableSlot& t = slots[cur_slot];  // still holds this scene's tables; launched() re-marks it
-      const int rc = blocks_upload();  // first: fill_frame reads d_cells
+      const int rc = blocks_upload(s);  // first: fill_frame reads d_cells
       if (rc != SFRT_OK) return rc;
+      HIP_TRY(grid.before_read(s));
       HIP_TRY(t.use_on(s));  // staged, or last read, on another stream: wait for it
       fill_frame(f, (uint8_t*)t.d, staged_off);
       return SFRT_OK;
@@ -264,8 +279,9 @@ struct sfrt_voxel {
     staged_off[0] = b_col;
     staged_off[1] = b_col + b_row;
     staged_off[2] = b_col + b_row + b_dyn;
-    const int rc = blocks_upload();  // first: fill_frame reads d_cells
+    const int rc = blocks_upload(s);  // first: fill_frame reads d_cells
     if (rc != SFRT_OK) return rc;
+    HIP_TRY(grid.before_read(s));
     fill_frame(f, (uint8_t*)t.d, staged_off);
     return SFRT_OK;
   }
@@ -273,26 +289,54 @@ struct sfrt_voxel {
   // The world as the kernel reads it: byte (x << 20) + (y << 10) + z = id + kVoxCellBias of the
   // block at (x, y, z), 0 elsewhere (the reference's map key as a linear index, voxel_trace.h).
   // nx planes of 1 MiB; each plane's ny rows of nz codes land at row pitch 1024.
-  int blocks_upload() {
-    if (blocks_dirty) {  // rare: launches on any stream may still read the old grid
-      HIP_TRY(hipDeviceSynchronize());
-      const size_t bytes = (size_t)nx << 20;
-      if (d_cells_cap < bytes) {
-        (void)hipFree(d_cells);
-        d_cells = nullptr;
-        d_cells_cap = 0;
-        HIP_TRY(hipMalloc(&d_cells, bytes));
-        d_cells_cap = bytes;
-      }
-      HIP_TRY(hipMemset(d_cells, 0, bytes));
-      std::vector<uint8_t> code(blocks.size());
-      for (size_t k = 0; k < blocks.size(); k++)
-        code[k] = blocks[k] == sfrt::kVoxEmpty ? 0 : (uint8_t)(blocks[k] + sfrt::kVoxCellBias);
-      for (int x = 0; x < nx; x++)
-        HIP_TRY(hipMemcpy2D(d_cells + ((size_t)x << 20), 1024, code.data() + (size_t)x * ny * nz,
-                            (size_t)nz, (size_t)nz, (size_t)ny, hipMemcpyHostToDevice));
-      blocks_dirty = false;
+  // Rare (the reference fills its map once, World.cpp:5-18) but stream-ordered like every other
+  // upload: the rewrite is queued on the frame's stream s behind every launch, on any stream, that
+  // read the old grid (SharedBuffer::before_write: device-side waits), and launches on other
+  // streams wait for it -- a frame of another world or renderer in flight is never held up.
+  // It writes only the box that holds the new world or anything an earlier one left non-zero.
+  int blocks_upload(hipStream_t s) {
+    if (!blocks_dirty) return SFRT_OK;
+    const size_t n = blocks.size();
+    if (codes_pending) {  // the staging buffers' last rewrite (queued by this object) has run
+      HIP_TRY(hipEventSynchronize(codes_ev));
+      codes_pending = false;
     }
+    HIP_TRY(grid.before_write(s));
+    if (codes_cap < n) {  // grows to the largest world seen (staging is not in use: above)
+      size_t cap = 1;
+      while (cap < n) cap <<= 1;
+      (void)hipHostFree(h_codes);
+      h_codes = nullptr;
+      if (d_codes) HIP_TRY(hipFreeAsync(d_codes, s));
+      d_codes = nullptr;
+      codes_cap = 0;
+      HIP_TRY(hipHostMalloc(&h_codes, cap, hipHostMallocDefault));
+      HIP_TRY(hipMallocAsync((void**)&d_codes, cap, s));
+      codes_cap = cap;
+    }
+    if (!codes_ev) HIP_TRY(hipEventCreateWithFlags(&codes_ev, hipEventDisableTiming));
+    const size_t bytes = (size_t)nx << 20;
+    if (d_cells_cap < bytes) {  // a fresh grid (stream-ordered on s), all zero
+      if (d_cells) HIP_TRY(hipFreeAsync(d_cells, s));
+      d_cells = nullptr;
+      d_cells_cap = 0;
+      HIP_TRY(hipMallocAsync((void**)&d_cells, bytes, s));
+      d_cells_cap = bytes;
+      HIP_TRY(hipMemsetAsync(d_cells, 0, bytes, s));
+      box[0] = box[1] = box[2] = 0;
+    }
+    for (size_t k = 0; k < n; k++)
+      h_codes[k] = blocks[k] == sfrt::kVoxEmpty ? 0 : (uint8_t)(blocks[k] + sfrt::kVoxCellBias);
+    HIP_TRY(hipMemcpyAsync(d_codes, h_codes, n, hipMemcpyHostToDevice, s));
+    // planes past the new nx are outside the kernel's buffer range, but a later, larger world
+    // would see them: the box covers them too while they may hold codes
+    const int bx = std::max(nx, box[0]), by = std::max(ny, box[1]), bz = std::max(nz, box[2]);
+    if (sfrt::launch_voxel_cells(d_cells, d_codes, nx, ny, nz, bx, by, bz, s)) return SFRT_E_HIP;
+    HIP_TRY(hipEventRecord(codes_ev, s));
+    codes_pending = true;
+    HIP_TRY(grid.after_write(s));
+    box[0] = nx; box[1] = ny; box[2] = nz;
+    blocks_dirty = false;
     return SFRT_OK;
   }
 
@@ -316,9 +360,10 @@ struct sfrt_voxel {
     f.status = d_status;
   }
 
-  // Marks the current table slot busy until the work queued on s completes.
+  // Marks the current table slot and the grid busy until the work queued on s completes.
   int launched(hipStream_t s) {
     HIP_TRY(slots[cur_slot].launched(s));
+    HIP_TRY(grid.after_read(s));
     return SFRT_OK;
   }
 
@@ -512,6 +557,7 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   f.tile_cost = p.tile_cost;
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
+  f.cost_diff = p.cost_diff ? 1 : 0;
   const bool queued = sfrt::launch_voxel(f, s) == 0;
   HIP_TRY(v->sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;

@@ -345,6 +345,7 @@ struct sfrt_world {
     f.tile_cost = p.tile_cost;
     f.prev_cost = p.prev_cost;
     f.next_order = p.next_order;
+    f.cost_diff = p.cost_diff ? 1 : 0;
     // a moving camera: the recorded classes are a frame or two off
     f.order_dilate = p.prev_cost && chain_last.valid &&
                      std::memcmp(&chain_last.cam, &cam, sizeof cam) != 0;
@@ -819,6 +820,7 @@ int sfrt_world_trace_points(sfrt_world* w, const int32_t* ij, int count, sfrt_pi
         f.tile_cost = p.tile_cost;
         f.prev_cost = p.prev_cost;
         f.next_order = p.next_order;
+        f.cost_diff = p.cost_diff ? 1 : 0;
       }
       const bool queued = sfrt::launch_trace(f, recs.data(), w->stream, &dump) == 0;
       if (w->tile_order_on) HIP_TRY(w->dump_sched.end(p, w->stream, queued));

@@ -421,11 +421,8 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     }
     slot -= 1;
   }
-  int tile = slot;
-  if (f.tile_order) {
-    const int t = (int)f.tile_order[slot];
-    tile = t < ntiles ? t : slot;  // never outside the grid
-  }
+  uint32_t cls;  // the tile's class in the order (sfrt_device.h slot_tile)
+  const int tile = slot_tile(f.tile_order, slot, ntiles, cls);
   const int tile_y = tile / f.tiles_x;  // f.tiles_x = ceil(sub_w / (8 R)) for this kernel
   const int tile_x = tile - tile_y * f.tiles_x;
   if (tile_y * kTile >= f.sub_rows) return;  // grid rounding; uniform per wave
@@ -639,7 +636,7 @@ __device__ __forceinline__ void trace_tile_window_r(const FrameRec& f,
     advance(L);
   }
   if (trips >= kMaxIterations && any_marching() && lane == 0) atomicOr(f.status, 1);
-  if (f.tile_cost && lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket((uint32_t)trips);
+  if (f.tile_cost && lane == 0) store_cost(f.tile_cost, tile, tile_bucket((uint32_t)trips), cls, f.cost_diff);
   // Pixel (a, b) of ray r, recomputed here from a fresh lane id (mbcnt, so that the
   // compiler does not reuse the kernel entry's values): kept from there, the columns sat
   // in registers through the whole march, and at R = 4 one of them was spilled.

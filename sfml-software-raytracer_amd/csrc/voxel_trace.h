@@ -85,10 +85,20 @@ struct VoxFrame {
   uint8_t* tile_cost;
   const uint8_t* prev_cost;
   uint32_t* next_order;
+  // tile_order's classes are the ones in tile_cost: store only changed classes (sfrt_device.h
+  // store_cost, sfrt_sched.h TileSchedPtrs::cost_diff)
+  int32_t cost_diff;
 };
 
 // Tile grid of launch_voxel for f (8x8 tiles): key (> 0) and tile count.
 long long voxel_tile_key(const VoxFrame& f, long long* tiles);
 int launch_voxel(const VoxFrame& f, void* stream);
+
+// Rewrites the key-indexed grid `cells` for a world of nx x ny x nz codes (`codes`, device,
+// x-major then y then z, as set_blocks takes them): every byte of planes x < bx, rows y < by,
+// columns z < bz gets its code inside the world and 0 outside it.  (bx, by, bz) covers the world
+// and every byte an earlier world may have left non-zero, so the grid is the new world's alone.
+int launch_voxel_cells(uint8_t* cells, const uint8_t* codes, int nx, int ny, int nz, int bx, int by,
+                       int bz, void* stream);
 
 }  // namespace sfrt

@@ -413,11 +413,8 @@ __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f
     }
     slot -= 1;
   }
-  int tile = slot;
-  if (f.tile_order) {
-    const int t = (int)f.tile_order[slot];
-    tile = t < ntiles ? t : slot;  // never outside the grid
-  }
+  uint32_t cls;  // the tile's class in the order (sfrt_device.h slot_tile)
+  const int tile = slot_tile(f.tile_order, slot, ntiles, cls);
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int a = tx * 8 + (lane & 7);
   const int b = f.sub_row0 + ty * 8 + (lane >> 3);
@@ -438,7 +435,30 @@ __global__ __launch_bounds__(64, SFRT_VOX_WAVES) void k_voxel_ordered(VoxFrame f
   if (COST) {
     // the tile's slowest ray, in DDA + shadow steps / 4 (the classes' scale)
     const uint32_t w = wave_max_u32(work);
-    if (lane == 0) f.tile_cost[tile] = (uint8_t)tile_bucket(w >> 2);
+    if (lane == 0) store_cost(f.tile_cost, tile, tile_bucket(w >> 2), cls, f.cost_diff);
+  }
+}
+
+// The grid rewrite of launch_voxel_cells: one 256-lane workgroup per (x, y) row of the box, four
+// bytes of the row per lane (a row starts at a 1 KiB boundary, so the full words are aligned
+// dword stores).
+__global__ __launch_bounds__(256) void k_voxel_cells(uint8_t* __restrict__ cells,
+                                                     const uint8_t* __restrict__ codes, int nx, int ny,
+                                                     int nz, int by, int bz) {
+  const int x = (int)blockIdx.x / by, y = (int)blockIdx.x - x * by;
+  const int z0 = 4 * (int)threadIdx.x;
+  if (z0 >= bz) return;
+  const bool row_in = x < nx && y < ny;
+  const uint8_t* src = codes + ((size_t)x * ny + y) * nz;
+  uint8_t b[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) b[k] = row_in && z0 + k < nz ? src[z0 + k] : (uint8_t)0;
+  uint8_t* dst = cells + ((size_t)x << 20) + ((size_t)y << 10) + z0;
+  if (z0 + 4 <= bz) {
+    *reinterpret_cast<uint32_t*>(dst) =
+        (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+  } else {
+    for (int k = 0; z0 + k < bz; k++) dst[k] = b[k];
   }
 }
 
@@ -455,7 +475,7 @@ long long voxel_tile_key(const VoxFrame& f, long long* tiles) {
 int launch_voxel(const VoxFrame& f, void* stream) {
   long long tiles = 0;
   if (voxel_tile_key(f, &tiles) == 0) return 0;
-  // the kernel reads the grid through a buffer resource over f.blocks and the tables
+  // the kernel reads the grid through a buffer resource over f.cells (f.cell_bytes) and the tables
   // unguarded: refuse a record whose device pointers were not filled
   if (!f.cells || f.cell_bytes == 0 || !f.col || !f.row || !f.out || !f.status ||
       (f.ndyn > 0 && !f.dyn) || (f.nlights > 0 && !f.lights))
@@ -468,6 +488,18 @@ int launch_voxel(const VoxFrame& f, void* stream) {
   else
     hipLaunchKernelGGL(k_voxel_ordered<false>, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64),
                        0, (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_voxel_cells(uint8_t* cells, const uint8_t* codes, int nx, int ny, int nz, int bx, int by,
+                       int bz, void* stream) {
+  // the box must hold the world and stay inside the key space (kVoxMax*), the rows inside 1 KiB
+  if (!cells || (nx > 0 && !codes) || nx < 0 || ny < 0 || nz < 0 || bx < nx || by < ny || bz < nz ||
+      bx > kVoxMaxX || by > kVoxMaxY || bz > kVoxMaxZ)
+    return -1;
+  if (bx == 0 || by == 0 || bz == 0) return 0;
+  hipLaunchKernelGGL(k_voxel_cells, dim3((unsigned)((long long)bx * by)), dim3(256), 0,
+                     (hipStream_t)stream, cells, codes, nx, ny, nz, by, bz);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

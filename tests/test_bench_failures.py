@@ -64,7 +64,9 @@ def test_supervisor_time_limit_ends_a_hung_run():
 
 def test_partial_line_keeps_a_measured_headline(tmp_path):
     """A failure after the headline: rank 0's supervisor prints the line the body had reached
-    (bench.py --partial-out), with the error, and exits 0 -- the headline is a measurement."""
+    (bench.py --partial-out), with the error and "complete": false, and exits PARTIAL_EXIT (4,
+    distinct from 0, from 1 = no headline and from 3 = frames differ), so the driver's status shows
+    the partial run.  The supervisor's signal handlers are restored after it."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
@@ -78,6 +80,8 @@ def test_partial_line_keeps_a_measured_headline(tmp_path):
         "           '_stage': 'after the headline'}, open(sys.argv[i + 1], 'w'))\n"
         "print('body: dying after the headline', file=sys.stderr)\n"
         "os._exit(9)\n")
+    import signal
+    handlers = {sg: signal.getsignal(sg) for sg in (signal.SIGTERM, signal.SIGINT)}
     old_file = bench.__file__
     bench.__file__ = str(fake)
     try:
@@ -89,7 +93,9 @@ def test_partial_line_keeps_a_measured_headline(tmp_path):
     finally:
         bench.__file__ = old_file
     lines = [ln for ln in out.getvalue().splitlines() if ln.startswith("{")]
-    assert rc == 0 and len(lines) == 1
+    assert bench.PARTIAL_EXIT not in (0, 1, 3)
+    assert rc == bench.PARTIAL_EXIT and len(lines) == 1
+    assert {sg: signal.getsignal(sg) for sg in handlers} == handlers
     line = json.loads(lines[0])
     assert line["value"] == 123.0 and line["complete"] is False
     assert line["error"]["stage"] == "after the headline" and line["error"]["exit"] == 9
@@ -108,3 +114,45 @@ def test_bit_identity_flags_found_everywhere():
     assert flags == {"frame_check/bit_identical": True, "gathered_frame_bit_identical": True,
                      "also/a/bit_identical": False, "also/c/candidates/x/bit_identical": True,
                      "also/h/pipelined_pinned/bit_identical_to_device_frame": True}
+
+
+def test_supervised_child_dies_with_its_supervisor(tmp_path):
+    """the body runs in its own session (start_new_session), out of reach of the group
+    signals torch.distributed.run sends; if the supervisor itself is SIGKILLed, the body must not
+    live on holding the GPU (PR_SET_PDEATHSIG in bench._die_with_parent)."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    fake = tmp_path / "sleepy_body.py"
+    pidfile = tmp_path / "child.pid"
+    fake.write_text("import os, sys, time\n"
+                    f"open({str(pidfile)!r}, 'w').write(str(os.getpid()))\n"
+                    "time.sleep(120)\n")
+    driver = ("import importlib.util, sys\n"
+              f"spec = importlib.util.spec_from_file_location('bench_mod', {os.path.join(ROOT, 'bench.py')!r})\n"
+              "bench = importlib.util.module_from_spec(spec); spec.loader.exec_module(bench)\n"
+              f"bench.__file__ = {str(fake)!r}\n"
+              "sys.exit(bench.supervise([], 1, 2, 300))\n")
+    sup = subprocess.Popen([sys.executable, "-c", driver])
+    try:
+        t0 = time.monotonic()
+        while not pidfile.exists() or not pidfile.read_text():
+            assert time.monotonic() - t0 < 60, "the body never started"
+            time.sleep(0.1)
+        pid = int(pidfile.read_text())
+        os.kill(sup.pid, signal.SIGKILL)
+        sup.wait(timeout=30)
+        t0 = time.monotonic()
+        while True:
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            if time.monotonic() - t0 > 20:
+                os.kill(pid, signal.SIGKILL)
+                raise AssertionError("the body outlived its SIGKILLed supervisor")
+            time.sleep(0.1)
+    finally:
+        if sup.poll() is None:
+            sup.kill()

@@ -373,6 +373,44 @@ def test_row_costs_equal_oracle_march_steps(floor_tex, name, width, height, pose
     w.close()
 
 
+def test_row_costs_exact_when_only_changed_classes_are_stored(floor_tex):
+    """The tile-order chain stores a tile's class only when it differs from the class its order
+    entry carries (sfrt_device.h store_cost; the entry was sorted from the very buffer the launch
+    records into).  Frame after frame with the camera turning, after a timing-probe launch (which
+    stores every class and breaks that match, TileSched::probed) and with the camera still again,
+    the recorded classes must stay every tile's class of ITS frame: the row costs equal the
+    oracle's for the pose of the last frame, after every frame."""
+    import oracle
+    import sfrt
+    import torch
+    from conftest import host_threads
+    width, height = 1920, 1080
+    poses = [(0.0, 0.0)] * 3 + [(0.04 * k, 0.01 * k) for k in range(1, 6)] + [(0.2, 0.05)] * 3
+    w = sfrt.World(0)
+    try:
+        w.load_texture(*floor_tex)
+        buf = torch.empty(height, width * 4, dtype=torch.uint8, device="cuda")
+        for k, pose in enumerate(poses + ["probe", (0.3, -0.1), (0.3, -0.1)]):
+            if pose == "probe":  # mode 2: reuses the last order, no sorter, stores every class
+                w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 2)
+                w.set_scene(scenes.SCENES["default10"]().posed(0.25, 0.0), width, height)
+                w.render_band(buf.data_ptr(), width * 4, 0, height)
+                w.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
+                continue
+            sc = scenes.SCENES["default10"]().posed(*pose)
+            w.set_scene(sc, width, height)
+            w.render_band(buf.data_ptr(), width * 4, 0, height)
+            if k < 2:
+                continue
+            r0, cost = w.row_costs()
+            it = oracle.Oracle.from_scene(sc, width, height, *floor_tex).iteration_map(host_threads())
+            np.testing.assert_array_equal(
+                cost, _expected_row_costs(it.reshape(height, width), width, 0, height), err_msg=str((k, pose)))
+        w.check()
+    finally:
+        w.close()
+
+
 @pytest.mark.parametrize("key,n,factor", [
     ("c4_7680x4320_lcg64@0,0", 4, 1.0), ("c4_7680x4320_default10@0,0", 2, 2.0)])
 def test_multi_balance_matches_golden(floor_tex, key, n, factor):

@@ -427,3 +427,84 @@ def test_random_worlds_oracle_deterministic(assets):
         a = o.render(8)
         assert oracle.VoxelOracle.bad_texel_reads() == before, seed
         assert np.array_equal(a, o.render(1)), seed
+
+
+@pytest.mark.gpu
+def test_voxel_blocks_rewrite_does_not_serialise_other_streams(built, assets):
+    """VERDICT r5 item 2 (sfrt_voxel.cpp blocks_upload, sfrt_host.h SharedBuffer): new blocks
+    while 4K sphere frames are in flight on stream A.  The voxel frame on stream B rewrites the
+    grid stream-ordered -- behind the voxel launches that read the old grid, not behind A -- so
+    the call returns and B's frame completes while A is still busy (the round-5 code's
+    hipDeviceSynchronize held both until A drained).  The rewritten grid's frames equal the
+    restatement: same dimensions, then smaller (the box of the old world cleared) and larger
+    (100 x 10 x 100: a new allocation) worlds, each rewrite queued on A with a frame of the old
+    world still queued on B."""
+    import time
+    import sfrt
+    import scenes
+    import torch
+    w, h = 320, 180
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    tex, tw, th = scenes.load_floor()
+    sphere = sfrt.World(0)
+    vworld = sfrt.VoxelWorld(0)  # its own grid: the first world allocates it, the last grows it
+    vworld.load_assets(assets[0], assets[1], vs.COLORS)
+    try:
+        sphere.load_texture(tex, tw, th)
+        sphere.set_scene(scenes.lcg64(), 3840, 2160)
+        frame4k = torch.empty((2160, 3840 * 4), dtype=torch.uint8, device="cuda:0")
+        sphere.render_band(frame4k.data_ptr(), 3840 * 4, 0, 2160, a.cuda_stream)  # warm
+        worlds = [vs.random_world(seed) for seed in (2, 9, 14)]
+        first, fw, fh = worlds[0]
+        vworld.set_scene(first, fw, fh)
+        warm = torch.empty((fh, fw * 4), dtype=torch.uint8, device="cuda:0")
+        vworld.render_band(warm.data_ptr(), fw * 4, 0, fh, b.cuda_stream)
+        vworld.check(b.cuda_stream)
+        torch.cuda.synchronize()
+        # same dimensions, new blocks: no allocation on the way
+        import dataclasses
+        blocks2 = first.blocks.copy()
+        textured = (blocks2 >= 0) & (blocks2 != vs.EMPTY)
+        blocks2[textured] = (blocks2[textured] + 1) % 4  # the same cells, other textures
+        second = dataclasses.replace(first, blocks=blocks2)
+        for _ in range(40):  # ~6 ms of sphere frames queued on A
+            sphere.render_band(frame4k.data_ptr(), 3840 * 4, 0, 2160, a.cuda_stream)
+        t0 = time.perf_counter()
+        vworld.set_scene(second, fw, fh)
+        got = torch.full((fh, fw * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        vworld.render_band(got.data_ptr(), fw * 4, 0, fh, b.cuda_stream)
+        done_b = torch.cuda.Event()
+        done_b.record(b)
+        call_s = time.perf_counter() - t0
+        a_busy_after_call = not a.query()
+        while not done_b.query():
+            pass
+        a_busy_after_b = not a.query()
+        torch.cuda.synchronize()
+        assert a_busy_after_call, f"the voxel call returned only after A drained ({call_s * 1e3:.2f} ms)"
+        assert a_busy_after_b, "B's voxel frame waited for the sphere frames on A"
+        vworld.check(b.cuda_stream)
+        want = oracle.VoxelOracle(second, fw, fh, assets[0], assets[1], vs.COLORS).render(host_threads())
+        assert np.array_equal(got.cpu().numpy().ravel(), want)
+        # smaller and larger worlds, the previous world's frame queued on B ahead of each rewrite
+        prev = (second, fw, fh)
+        for scene, sw, sh in worlds[1:] + [(vs.default_world(), 320, 180)]:
+            vworld.set_scene(prev[0], prev[1], prev[2])
+            old = torch.full((prev[2], prev[1] * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            with torch.cuda.stream(b):
+                torch.cuda._sleep(20_000_000)  # the old world's frame still queued behind this
+            vworld.render_band(old.data_ptr(), prev[1] * 4, 0, prev[2], b.cuda_stream)
+            vworld.set_scene(scene, sw, sh)
+            new = torch.full((sh, sw * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            vworld.render_band(new.data_ptr(), sw * 4, 0, sh, a.cuda_stream)  # rewrite on A
+            torch.cuda.synchronize()
+            vworld.check(a.cuda_stream)
+            vworld.check(b.cuda_stream)
+            for sc, ww, hh, buf in ((prev[0], prev[1], prev[2], old), (scene, sw, sh, new)):
+                want = oracle.VoxelOracle(sc, ww, hh, assets[0], assets[1], vs.COLORS).render(
+                    host_threads())
+                assert np.array_equal(buf.cpu().numpy().ravel(), want), (ww, hh, sc.blocks.shape)
+            prev = (scene, sw, sh)
+    finally:
+        sphere.close()
+        vworld.close()

@@ -1,6 +1,7 @@
-# Round-5 A/B call: voxel and GLSL library A/Bs, the GPU tests of each candidate, and block counts
-# of instrumented variants, under gpurun_out/$TAG/:
-#   VLIBS=a.so,b.so VCAND=b.so GLIBS=a.so,c.so GCAND=c.so BB="voxel:ll glsl:gl" TAG=r5d bash tools/gpu/ab_r5.sh
+# A/B of prebuilt libraries per renderer (VLIBS voxel, GLIBS GLSL, SLIBS sphere), the GPU tests of
+# each candidate (VCAND, GCAND, SCAND) and block counts of instrumented variants (BB="kernel:variant";
+# tools/isa_block_profile.py), under gpurun_out/$TAG/:
+#   VLIBS=a.so,b.so VCAND=b.so GLIBS=a.so,c.so GCAND=c.so BB="voxel:base glsl:gl" TAG=r6x bash tools/gpu/ab_kernels.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # alternating (profiles/ab/r5_ab9):  /usr/local/graft/bin/gpurun -- "bash tools/gpu/kernarg_ab.sh"
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r5o
+O=gpurun_out/${TAG:-kernarg}
 mkdir -p $O
 for i in 1 2; do
   for v in unset 1 0; do
