@@ -81,6 +81,7 @@ struct GlslFrame {
 
 // Tile grid of the ordered GLSL kernel for f: key (> 0) and tile count.
 long long glsl_tile_key(const GlslFrame& f, long long* tiles);
-int launch_glsl(const GlslFrame& f, void* stream);
+// done_event (hipEvent_t, may be null): recorded by the launch's own completion (its stop event).
+int launch_glsl(const GlslFrame& f, void* stream, void* done_event = nullptr);
 
 }  // namespace sfrt

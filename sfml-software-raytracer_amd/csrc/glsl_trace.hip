@@ -10,6 +10,7 @@
 // (oracle/glsl_oracle.c) bit for bit.  Every expression keeps the shader's
 // operand order.  Sphere data are wave-uniform (scalar loads); only the
 // per-fragment lookups by drawSphere (:123-125, :154) are vector loads.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "glsl_trace.h"
@@ -470,17 +471,18 @@ long long glsl_tile_key(const GlslFrame& f, long long* tiles) {
   return (1ll << 62) | ((long long)f.tiles_x << 28) | ty;
 }
 
-int launch_glsl(const GlslFrame& f, void* stream) {
+int launch_glsl(const GlslFrame& f, void* stream, void* done_event) {
   const int tiles_y = (f.rows + 7) / 8;
   const long long tiles = (long long)f.tiles_x * tiles_y;
   if (tiles == 0) return 0;
   if (f.tile_cost) {  // adaptive tile order (the host linked this launch into its chain)
     if (tiles > 0x7ffffffeLL) return -1;
-    hipLaunchKernelGGL(k_glsl_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,
-                       (hipStream_t)stream, f, (int)tiles);
+    hipExtLaunchKernelGGL(k_glsl_ordered, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64), 0,
+                          (hipStream_t)stream, nullptr, (hipEvent_t)done_event, 0, f, (int)tiles);
     return hipGetLastError() != hipSuccess;
   }
-  hipLaunchKernelGGL(k_glsl, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, (hipStream_t)stream, f);
+  hipExtLaunchKernelGGL(k_glsl, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                        nullptr, (hipEvent_t)done_event, 0, f);
   return hipGetLastError() != hipSuccess;
 }
 

@@ -317,11 +317,10 @@ struct sfrt_glsl {
     f.status = d_status;
   }
 
-  // Marks the current table slot busy until the work queued on s completes.
-  int launched(hipStream_t s) {
-    HIP_TRY(slots[cur_slot].launched(s));
-    return SFRT_OK;
-  }
+  // The current table slot's event, for the launch that reads it to record (its stop event:
+  // sfrt_host.h TableSlot::launch_event), and the slot marked busy once that launch is queued.
+  void* launch_event() const { return slots[cur_slot].launch_event(); }
+  void launched(hipStream_t s) { slots[cur_slot].launched_with(s); }
 
   int read_status(hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
@@ -480,10 +479,11 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
   f.cost_diff = p.cost_diff ? 1 : 0;
-  const bool queued = sfrt::launch_glsl(f, s) == 0;
+  const bool queued = sfrt::launch_glsl(f, s, g->launch_event()) == 0;
   HIP_TRY(g->sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;
-  return g->launched(s);
+  g->launched(s);
+  return SFRT_OK;
 }
 
 int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
@@ -509,8 +509,8 @@ int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
   f.tiles_x = (width + 7) / 8;
   f.out = g->d_frame;
   f.out_pitch = width;
-  if (sfrt::launch_glsl(f, g->stream)) return SFRT_E_HIP;
-  if ((rc = g->launched(g->stream))) return rc;
+  if (sfrt::launch_glsl(f, g->stream, g->launch_event())) return SFRT_E_HIP;
+  g->launched(g->stream);
   HIP_TRY(hipMemcpyAsync(pixels, g->d_frame, px * 4, hipMemcpyDeviceToHost, g->stream));
   return g->read_status(g->stream);
 }

@@ -57,6 +57,15 @@ struct TableSlot {
   }
   // After queuing a launch on s that reads the slot (use_on(s) came first).
   hipError_t launched(hipStream_t s) { return mark(s); }
+  // The same through the launch itself: the event to pass to the kernel launch as its stop event
+  // (hipExtLaunchKernelGGL: the dispatch packet's own completion signal records it, so no marker
+  // packet sits between two frames -- a hipEventRecord after every launch cost the 1080p voxel
+  // frame ~5 us, profiles/ab/r6_ab3), then launched_with(s) once the launch is queued on s.
+  hipEvent_t launch_event() const { return ev; }
+  void launched_with(hipStream_t s) {
+    last = s;
+    pending = true;
+  }
   void release() {
     (void)hipFree(d);
     (void)hipHostFree(h);
@@ -79,56 +88,45 @@ struct TableSlot {
 
 // A device buffer that every launch reads, on whatever stream, and that is rewritten in place now
 // and then (the voxel grid, sfrt_voxel.cpp): stream-ordered both ways, with no host or device-wide
-// synchronisation.  One event per reading stream, re-recorded after each launch on it; a rewrite
-// queued on stream w first makes w wait for each of them on the device (hipStreamWaitEvent), and
-// records `written` after itself, which the next launch on each other stream waits for once.
+// synchronisation and no per-frame work.  Every launch that reads the buffer also reads a table
+// slot and re-records the slot's event, which by TableSlot's rule covers every earlier user of the
+// slot; so a rewrite queued on stream w is ordered after every reader by w waiting, on the device,
+// for each pending slot event (and for the previous rewrite).  `written`, recorded after the
+// rewrite, orders the first later launch on each other stream after it.  (A second event recorded
+// after every launch, one per reading stream, had cost the 1080p voxel frame 5 us: ab/r6_ab3.)
 struct SharedBuffer {
-  struct Reader {
-    hipStream_t s = nullptr;
-    hipEvent_t ev = nullptr;
-    bool read = false;     // ev covers a launch that read the current contents
-    bool current = false;  // s is ordered after the last rewrite
-  };
-  std::vector<Reader> readers;
   hipEvent_t written = nullptr;
   hipStream_t writer = nullptr;
   bool have_written = false;
+  std::vector<hipStream_t> current;  // other streams already ordered after the last rewrite
 
   // Before queuing a launch on s that reads the buffer.
   hipError_t before_read(hipStream_t s) {
-    Reader* r = nullptr;
-    const hipError_t e = reader(s, &r);
+    if (!have_written || s == writer) return hipSuccess;
+    for (hipStream_t c : current)
+      if (c == s) return hipSuccess;
+    const hipError_t e = hipStreamWaitEvent(s, written, 0);
     if (e != hipSuccess) return e;
-    if (have_written && !r->current && s != writer) {
-      const hipError_t w = hipStreamWaitEvent(s, written, 0);
-      if (w != hipSuccess) return w;
-    }
-    r->current = true;
+    if (current.size() >= 64) current.clear();  // (a forgotten stream only waits once more)
+    current.push_back(s);
     return hipSuccess;
   }
-  // After queuing that launch.
-  hipError_t after_read(hipStream_t s) {
-    Reader* r = nullptr;
-    hipError_t e = reader(s, &r);
-    if (e != hipSuccess) return e;
-    if ((e = hipEventRecord(r->ev, s)) != hipSuccess) return e;
-    r->read = true;
-    return hipSuccess;
-  }
-  // Before queuing a rewrite on w: w waits, on the device, for every launch that read the buffer.
-  hipError_t before_write(hipStream_t w) {
-    if (have_written && writer != w) {  // and for the last rewrite, if no read came between
+  // Before queuing a rewrite on w: w waits for every launch that read the buffer, through the
+  // table slots those launches read.
+  template <int N>
+  hipError_t before_write(hipStream_t w, const TableSlot (&readers)[N]) {
+    if (have_written && writer != w) {
       const hipError_t e = hipStreamWaitEvent(w, written, 0);
       if (e != hipSuccess) return e;
     }
-    for (Reader& r : readers)
-      if (r.read && r.s != w) {
-        const hipError_t e = hipStreamWaitEvent(w, r.ev, 0);
+    for (const TableSlot& t : readers)
+      if (t.pending && t.last != w) {
+        const hipError_t e = hipStreamWaitEvent(w, t.ev, 0);
         if (e != hipSuccess) return e;
       }
     return hipSuccess;
   }
-  // After queuing the rewrite on w: later launches on other streams wait for it.
+  // After queuing the rewrite on w.
   hipError_t after_write(hipStream_t w) {
     hipError_t e;
     if (!written && (e = hipEventCreateWithFlags(&written, hipEventDisableTiming)) != hipSuccess)
@@ -136,50 +134,14 @@ struct SharedBuffer {
     if ((e = hipEventRecord(written, w)) != hipSuccess) return e;
     writer = w;
     have_written = true;
-    for (Reader& r : readers) {
-      r.current = r.s == w;
-      r.read = false;  // the rewrite on w came after each of them
-    }
+    current.clear();
     return hipSuccess;
   }
   void release() {
-    for (Reader& r : readers)
-      if (r.ev) (void)hipEventDestroy(r.ev);
-    readers.clear();
     if (written) (void)hipEventDestroy(written);
     written = nullptr;
     have_written = false;
-  }
-
- private:
-  static constexpr size_t kMaxReaders = 16;
-  hipError_t reader(hipStream_t s, Reader** out) {
-    for (Reader& r : readers)
-      if (r.s == s) {
-        *out = &r;
-        return hipSuccess;
-      }
-    if (readers.size() >= kMaxReaders) {  // forget streams whose last read has completed
-      for (size_t k = readers.size(); k-- > 0;)
-        if (!readers[k].read || hipEventQuery(readers[k].ev) == hipSuccess) {
-          (void)hipEventDestroy(readers[k].ev);
-          readers.erase(readers.begin() + (long)k);
-        }
-      if (readers.size() >= kMaxReaders) {  // all busy: wait for the oldest
-        const hipError_t e = hipEventSynchronize(readers.front().ev);
-        if (e != hipSuccess) return e;
-        (void)hipEventDestroy(readers.front().ev);
-        readers.erase(readers.begin());
-      }
-    }
-    Reader r;
-    r.s = s;
-    const hipError_t e = hipEventCreateWithFlags(&r.ev, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
-    // a stream new to the buffer is ordered after the last rewrite once before_read has run
-    readers.push_back(r);
-    *out = &readers.back();
-    return hipSuccess;
+    current.clear();
   }
 };
 

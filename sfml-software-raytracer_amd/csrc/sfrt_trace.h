@@ -103,8 +103,10 @@ struct DumpArgs {
 };
 
 // sphere_trace.hip.  dump != nullptr: the DUMP instantiation of the kernel the table picks.
+// done_event (hipEvent_t, may be null): recorded by the list kernel's own completion (its stop
+// event; the inline kernel, which reads no device records, takes none).
 int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream,
-                 const DumpArgs* dump = nullptr);
+                 const DumpArgs* dump = nullptr, void* done_event = nullptr);
 // "release" for the shipped build; "diagnostic" (-DSFRT_EXP: wrong bytes by design) or
 // "ab" (EXTRA build flags, tools/ab_libs.py) otherwise.
 const char* trace_build_flavour();

@@ -138,7 +138,7 @@ struct sfrt_voxel {
   size_t codes_cap = 0;
   hipEvent_t codes_ev = nullptr;
   bool codes_pending = false;
-  sfrt::SharedBuffer grid;   // the launches reading d_cells, on every stream (sfrt_host.h)
+  sfrt::SharedBuffer grid;   // d_cells' rewrites ordered against its readers (sfrt_host.h)
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
   // launches on different streams never see a table overwritten under them.
@@ -301,7 +301,7 @@ struct sfrt_voxel {
       HIP_TRY(hipEventSynchronize(codes_ev));
       codes_pending = false;
     }
-    HIP_TRY(grid.before_write(s));
+    HIP_TRY(grid.before_write(s, slots));
     if (codes_cap < n) {  // grows to the largest world seen (staging is not in use: above)
       size_t cap = 1;
       while (cap < n) cap <<= 1;
@@ -360,12 +360,11 @@ struct sfrt_voxel {
     f.status = d_status;
   }
 
-  // Marks the current table slot and the grid busy until the work queued on s completes.
-  int launched(hipStream_t s) {
-    HIP_TRY(slots[cur_slot].launched(s));
-    HIP_TRY(grid.after_read(s));
-    return SFRT_OK;
-  }
+  // The current table slot's event, for the launch that reads it to record (its stop event), and
+  // the slot marked busy once that launch is queued on s (the event also covers the launch's
+  // read of the grid: SharedBuffer).
+  void* launch_event() const { return slots[cur_slot].launch_event(); }
+  void launched(hipStream_t s) { slots[cur_slot].launched_with(s); }
 
   int read_status(hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
@@ -517,8 +516,8 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   f.sub_rows = sub_h;
   f.out = v->d_frame;
   f.out_pitch = sub_w;
-  if (sfrt::launch_voxel(f, v->stream)) return SFRT_E_HIP;
-  if ((rc = v->launched(v->stream))) return rc;
+  if (sfrt::launch_voxel(f, v->stream, v->launch_event())) return SFRT_E_HIP;
+  v->launched(v->stream);
   std::vector<uint32_t> stage(px);
   HIP_TRY(hipMemcpyAsync(stage.data(), v->d_frame, px * 4, hipMemcpyDeviceToHost, v->stream));
   rc = v->read_status(v->stream);
@@ -558,10 +557,11 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
   f.cost_diff = p.cost_diff ? 1 : 0;
-  const bool queued = sfrt::launch_voxel(f, s) == 0;
+  const bool queued = sfrt::launch_voxel(f, s, v->launch_event()) == 0;
   HIP_TRY(v->sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;
-  return v->launched(s);
+  v->launched(s);
+  return SFRT_OK;
 }
 
 int sfrt_voxel_set_option(sfrt_voxel* v, int option, int value) {

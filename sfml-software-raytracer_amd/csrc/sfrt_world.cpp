@@ -328,6 +328,15 @@ struct sfrt_world {
     staged = -1;
     return SFRT_OK;
   }
+  // The same through the launch itself: the staged slot's event for launch_trace to record as
+  // the kernel's stop event (no marker packet between frames, sfrt_host.h
+  // TableSlot::launch_event), then launched_with() once the launch is queued.
+  void* ring_event() const { return staged >= 0 ? spheres_ev[staged] : nullptr; }
+  void launched_with() {
+    if (staged < 0) return;
+    spheres_pending[staged] = true;
+    staged = -1;
+  }
 
   // Before a render_band / submit_frame launch on s: link f into the tile-order chain.
   int sched_begin(sfrt::FrameRec& f, hipStream_t s) {
@@ -696,8 +705,8 @@ int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart, int yadd
   f.out_pitch = sub_w;
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
-  if (sfrt::launch_trace(f, recs.data(), w->stream)) return SFRT_E_HIP;
-  if ((rc = w->launched(w->stream))) return rc;
+  if (sfrt::launch_trace(f, recs.data(), w->stream, nullptr, w->ring_event())) return SFRT_E_HIP;
+  w->launched_with();
   HIP_TRY(hipMemcpyAsync(w->h_stage, w->d_frame, px * 4, hipMemcpyDeviceToHost, w->stream));
   rc = w->read_status(w->stream);
   if (rc) return rc;
@@ -743,8 +752,10 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   rc = w->stage_spheres(f, recs, s, false);
   if (rc) return rc;
   if ((rc = w->sched_begin(f, s))) return rc;
-  if ((rc = w->sched_end(f, s, sfrt::launch_trace(f, recs.data(), s) == 0))) return rc;
-  return w->launched(s);
+  if ((rc = w->sched_end(f, s, sfrt::launch_trace(f, recs.data(), s, nullptr, w->ring_event()) == 0)))
+    return rc;
+  w->launched_with();
+  return SFRT_OK;
 }
 
 int sfrt_world_check(sfrt_world* w, void* hip_stream) {
@@ -893,9 +904,10 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
   if ((rc = w->sched_begin(f, w->stream))) return rc;  // adaptive tile order, as render_band
-  if ((rc = w->sched_end(f, w->stream, sfrt::launch_trace(f, recs.data(), w->stream) == 0)))
+  if ((rc = w->sched_end(f, w->stream,
+                         sfrt::launch_trace(f, recs.data(), w->stream, nullptr, w->ring_event()) == 0)))
     return rc;
-  if ((rc = w->launched(w->stream))) return rc;
+  w->launched_with();
   HIP_TRY(hipEventRecord(slot.rendered, w->stream));
   HIP_TRY(hipStreamWaitEvent(w->copy_stream, slot.rendered, 0));
   HIP_TRY(hipMemcpyAsync(pixels, slot.d_buf, px * 4, hipMemcpyDeviceToHost, w->copy_stream));

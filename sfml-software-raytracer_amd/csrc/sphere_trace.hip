@@ -19,6 +19,7 @@
 //    for any ray of the tile (cone test with margins, below); the surviving
 //    spheres are visited in their original order, so "last passing index"
 //    (drawSphere, :368) and the max (:367) are unchanged.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "sfrt_device.h"
@@ -768,7 +769,7 @@ long long trace_tile_key(const FrameRec& f, long long* tiles) {
 }
 
 int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream,
-                 const DumpArgs* dump) {
+                 const DumpArgs* dump, void* done_event) {
   const long long tiles_y = (f.sub_rows + kTile - 1) / kTile;
   if (tiles_y <= 0 || f.sub_w <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -815,11 +816,12 @@ int launch_trace(const FrameRec& f, const SphereRec* host_spheres, void* stream,
       default: hipLaunchKernelGGL(k_trace_window_list_dump<4>, gr, b, 0, s, g, *dump); break;
     }
   } else {
+    const hipEvent_t ev = (hipEvent_t)done_event;  // the record ring's slot (sfrt_world.cpp)
     switch (rays) {
-      case 1: hipLaunchKernelGGL(k_trace_window_list<1>, gr, b, 0, s, g); break;
-      case 2: hipLaunchKernelGGL(k_trace_window_list<2>, gr, b, 0, s, g); break;
-      case 3: hipLaunchKernelGGL(k_trace_window_list<3>, gr, b, 0, s, g); break;
-      default: hipLaunchKernelGGL(k_trace_window_list<4>, gr, b, 0, s, g); break;
+      case 1: hipExtLaunchKernelGGL(k_trace_window_list<1>, gr, b, 0, s, nullptr, ev, 0, g); break;
+      case 2: hipExtLaunchKernelGGL(k_trace_window_list<2>, gr, b, 0, s, nullptr, ev, 0, g); break;
+      case 3: hipExtLaunchKernelGGL(k_trace_window_list<3>, gr, b, 0, s, nullptr, ev, 0, g); break;
+      default: hipExtLaunchKernelGGL(k_trace_window_list<4>, gr, b, 0, s, nullptr, ev, 0, g); break;
     }
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -92,7 +92,8 @@ struct VoxFrame {
 
 // Tile grid of launch_voxel for f (8x8 tiles): key (> 0) and tile count.
 long long voxel_tile_key(const VoxFrame& f, long long* tiles);
-int launch_voxel(const VoxFrame& f, void* stream);
+// done_event (hipEvent_t, may be null): recorded by the launch's own completion (its stop event).
+int launch_voxel(const VoxFrame& f, void* stream, void* done_event = nullptr);
 
 // Rewrites the key-indexed grid `cells` for a world of nx x ny x nz codes (`codes`, device,
 // x-major then y then z, as set_blocks takes them): every byte of planes x < bx, rows y < by,

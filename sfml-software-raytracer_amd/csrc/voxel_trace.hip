@@ -6,6 +6,7 @@
 // expression order, -ffp-contract=off, correctly rounded division and sqrt,
 // and the x86-64 float->integer conversions of the reference's build
 // (out-of-range and NaN give INT_MIN / 0) emulated explicitly.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "sfrt_device.h"
@@ -472,7 +473,7 @@ long long voxel_tile_key(const VoxFrame& f, long long* tiles) {
   return (1ll << 62) | (tx << 28) | ty;
 }
 
-int launch_voxel(const VoxFrame& f, void* stream) {
+int launch_voxel(const VoxFrame& f, void* stream, void* done_event) {
   long long tiles = 0;
   if (voxel_tile_key(f, &tiles) == 0) return 0;
   // the kernel reads the grid through a buffer resource over f.cells (f.cell_bytes) and the tables
@@ -482,12 +483,13 @@ int launch_voxel(const VoxFrame& f, void* stream) {
     return -1;
   if (tiles > 0x7ffffffeLL) return -1;
   // row-major unless the host linked this launch into its tile-order chain
+  const dim3 grid((unsigned)(tiles + (f.prev_cost ? 1 : 0)));
   if (f.tile_cost)
-    hipLaunchKernelGGL(k_voxel_ordered<true>, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64),
-                       0, (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
+    hipExtLaunchKernelGGL(k_voxel_ordered<true>, grid, dim3(64), 0, (hipStream_t)stream, nullptr,
+                          (hipEvent_t)done_event, 0, f, (int)((f.sub_w + 7) / 8), (int)tiles);
   else
-    hipLaunchKernelGGL(k_voxel_ordered<false>, dim3((unsigned)(tiles + (f.prev_cost ? 1 : 0))), dim3(64),
-                       0, (hipStream_t)stream, f, (int)((f.sub_w + 7) / 8), (int)tiles);
+    hipExtLaunchKernelGGL(k_voxel_ordered<false>, grid, dim3(64), 0, (hipStream_t)stream, nullptr,
+                          (hipEvent_t)done_event, 0, f, (int)((f.sub_w + 7) / 8), (int)tiles);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

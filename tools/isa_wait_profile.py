@@ -17,9 +17,13 @@ accumulators are added to a device array at s_endpgm.  Each site therefore costs
 stamp's latency (the calibration lanes measure it, at the wave's start and end, as a stamp pair
 around an `lgkmcnt(0)` with nothing else outstanding).  A site with `lgkmcnt(k)`, k > 0, waits
 for lgkmcnt(k + 1) instead (the stamp is the youngest scalar request; such sites only ever count
-in-order requests).  Lanes 0-3: the wave's lifetime (end stamp minus entry stamp), the
-calibration pair at the end and at the start, and the number of waves.  At most 4 spare VGPRs
-are used (the headline kernel has 60: 64 keep 8 waves per SIMD), so at most 252 sites.
+in-order requests).  Lanes 0-4: the wave's lifetime (end stamp minus entry stamp), the
+calibration pair at the end and at the start, the number of waves, and the drain of the wave's
+last stores before s_endpgm (which the release kernel's s_endpgm waits for implicitly).  At most 4 spare VGPRs
+are used (the headline kernel has 60: 64 keep 8 waves per SIMD), so at most 251 sites.  Each wave
+adds its lanes into the copy of its CU (XCC_ID and HW_ID), not into one array for the whole chip:
+32,400 waves' atomics on the same two cache lines had tripled the kernel's time and queued its
+own loads behind them.
 
 `report` divides each site's cycles by its executions (the block counts of the same tree's
 tools/isa_block_profile.py build) and sums cycles by the source regions of
@@ -38,8 +42,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import isa_block_profile as ibp  # noqa: E402
 
 TAG = "waits"
-RESERVED = 4  # lanes: lifetime, calibration at the end, calibration at the start, waves
+RESERVED = 5  # lanes: lifetime, calibration at the end and at the start, waves, end drain
 MAX_VGPRS = 4
+COPIES = 1024  # one accumulator copy per CU: XCC_ID (3 bits) and HW_ID's cu / sh / se (7 bits)
+LANES = 64 * MAX_VGPRS
 
 
 def excluded(chain_list, rare):
@@ -116,13 +122,24 @@ def instrument(lines, symbol, sites):
                       [f"\ts_cmp_lg_u32 s{sS}, 0"])
     for i in range(st + 1, en):
         if lines[i].strip().startswith("s_endpgm"):
-            end = ["\ts_waitcnt vmcnt(0) lgkmcnt(0)"] + stamp_pair(1) + \
+            # the drain of the wave's last stores (s_endpgm's implicit wait in the release
+            # kernel), timed like a site into lane 4
+            end = [f"\ts_memtime s[{sA}:{sA + 1}]", "\ts_waitcnt vmcnt(0) lgkmcnt(0)",
+                   f"\ts_memtime s[{sB}:{sB + 1}]", "\ts_waitcnt lgkmcnt(0)",
+                   f"\ts_sub_u32 s{sT}, s{sB}, s{sA}"] + acc_add(4, f"s{sT}") + stamp_pair(1) + \
                   [f"\ts_memtime s[{sA}:{sA + 1}]", "\ts_waitcnt lgkmcnt(0)"] + \
                   acc_add(0, f"s{sA}") + acc_add(3, "1")
             flush = ["\ts_mov_b64 exec, -1",
                      "\tv_mbcnt_lo_u32_b32 v0, -1, 0",
                      "\tv_mbcnt_hi_u32_b32 v0, -1, v0",
                      "\tv_lshlrev_b32_e32 v0, 2, v0",
+                     # the CU's copy: (XCC_ID << 7 | HW_ID[14:8]) * LANES * 4 bytes
+                     f"\ts_getreg_b32 s{sT}, hwreg(HW_REG_XCC_ID, 0, 3)",
+                     f"\ts_getreg_b32 s{sU}, hwreg(HW_REG_HW_ID, 8, 7)",
+                     f"\ts_lshl_b32 s{sT}, s{sT}, 7",
+                     f"\ts_or_b32 s{sT}, s{sT}, s{sU}",
+                     f"\ts_mul_i32 s{sT}, s{sT}, {LANES * 4}",
+                     f"\tv_add_u32_e32 v0, s{sT}, v0",
                      "\ts_getpc_b64 s[0:1]",
                      f"\ts_add_u32 s0, s0, {ibp.COUNTERS}@rel32@lo+4",
                      f"\ts_addc_u32 s1, s1, {ibp.COUNTERS}@rel32@hi+12",
@@ -148,6 +165,32 @@ def instrument(lines, symbol, sites):
     return "\n".join(out), nl
 
 
+def patch_source(src_text):
+    """The per-CU accumulator copies and a reader summing them (sfrt_bbprof_read's signature,
+    so tools/isa_block_profile.py run reads them)."""
+    return src_text + f"""
+
+// ---- isa_wait_profile.py instrumentation (copy only) ----
+__device__ unsigned int {ibp.COUNTERS}[{COPIES * LANES}];
+extern "C" __attribute__((visibility("default"))) int sfrt_bbprof_read(unsigned int* out, int reset) {{
+  static unsigned int h[{COPIES * LANES}];
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL({ibp.COUNTERS}), sizeof h) != hipSuccess) return -1;
+  for (int l = 0; l < {LANES}; l++) {{  // 64-bit sums as (low, high) words
+    unsigned long long t = 0;
+    for (int c = 0; c < {COPIES}; c++) t += h[c * {LANES} + l];
+    out[2 * l] = (unsigned int)t;
+    out[2 * l + 1] = (unsigned int)(t >> 32);
+  }}
+  if (reset) {{
+    for (auto& x : h) x = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL({ibp.COUNTERS}), h, sizeof h) != hipSuccess) return -1;
+  }}
+  return 0;
+}}
+"""
+
+
 def build(kind):
     """The timed copy, through isa_block_profile.build's pipeline with this instrumentation."""
     ibp.VARIANT["tag"] = TAG
@@ -163,14 +206,14 @@ def build(kind):
         txt, nl = instrument(lines, symbol, sites)
         state.update(sites=[{"line": i, "block": b, "text": t} for i, b, t in sites],
                      skipped=skipped, lanes=nl)
-        return txt, [None] * nl  # isa_block_profile.build records len() as the lane count
+        return txt, [None] * (2 * nl)  # isa_block_profile.build records len(): two words a lane
 
-    saved = ibp.instrument
-    ibp.instrument = timed
+    saved = ibp.instrument, ibp.patch_source
+    ibp.instrument, ibp.patch_source = timed, patch_source
     try:
         ibp.build(kind)
     finally:
-        ibp.instrument = saved
+        ibp.instrument, ibp.patch_source = saved
     info_p = os.path.join(ibp.base(kind), "info.json")
     info = json.load(open(info_p))
     info.update(state)
@@ -211,7 +254,8 @@ def report(kind, waits_path, counts_path, pmc_path):
            "waits": os.path.relpath(waits_path, ibp.ROOT),
            "counts": os.path.relpath(counts_path, ibp.ROOT), "launches": {}}
     for key, ent in waits["launches"].items():
-        lanes = ent["block_executions_per_launch"]
+        w = ent["block_executions_per_launch"]  # (low, high) words of each lane's sum
+        lanes = [w[2 * i] + w[2 * i + 1] * 4294967296.0 for i in range(len(w) // 2)]
         ex = counts["launches"][key]["block_executions_per_launch"]
         if len(ex) != len(blocks):
             raise SystemExit("block counts for a different block table")
@@ -238,6 +282,8 @@ def report(kind, waits_path, counts_path, pmc_path):
             d["cycles_per_launch"] = round(d["cycles_per_launch"])
             d["executions_per_launch"] = round(d["executions_per_launch"], 1)
         row = {"frame": ent["frame"], "waves": round(waves, 1),
+               "end_store_drain_cycles_mean": round(lanes[4] / waves, 1),
+               "end_store_drain_share_of_lifetime": round(lanes[4] / life, 5),
                "wave_lifetime_cycles_mean": round(life / waves, 1),
                "stamp_pair_cycles_start": round(cal_start, 1),
                "stamp_pair_cycles_end": round(cal_end, 1),
