@@ -131,13 +131,19 @@ struct sfrt_voxel {
   // Every byte of d_cells outside planes x < box[0], rows y < box[1], columns z < box[2] is 0.
   int box[3] = {0, 0, 0};
   bool blocks_dirty = true;
-  // The codes of the last set_blocks on their way to the grid: pinned staging, its device copy,
-  // and the event after the last rewrite that read them (the next upload reuses both).
-  uint8_t* h_codes = nullptr;
-  uint8_t* d_codes = nullptr;
-  size_t codes_cap = 0;
-  hipEvent_t codes_ev = nullptr;
-  bool codes_pending = false;
+  // The codes of a set_blocks on their way to the grid: pinned staging, its device copy, and the
+  // event after the rewrite that read them.  Two in turn, so that blocks set on consecutive frames
+  // do not wait on the host for the previous rewrite (which may sit behind other work on its
+  // stream); an upload reuses a pair only after that pair's previous rewrite has run.
+  struct CodeStage {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  };
+  CodeStage stage[2];
+  int stage_next = 0;
   sfrt::SharedBuffer grid;   // d_cells' rewrites ordered against its readers (sfrt_host.h)
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
@@ -169,9 +175,11 @@ struct sfrt_voxel {
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
     (void)hipFree(d_cells);
-    (void)hipFree(d_codes);
-    (void)hipHostFree(h_codes);
-    if (codes_ev) (void)hipEventDestroy(codes_ev);
+    for (CodeStage& c : stage) {
+      (void)hipFree(c.d);
+      (void)hipHostFree(c.h);
+      if (c.ev) (void)hipEventDestroy(c.ev);
+    }
     grid.release();
     for (auto& t : slots) t.release();
     (void)hipFree(d_status);
@@ -297,24 +305,25 @@ struct sfrt_voxel {
   int blocks_upload(hipStream_t s) {
     if (!blocks_dirty) return SFRT_OK;
     const size_t n = blocks.size();
-    if (codes_pending) {  // the staging buffers' last rewrite (queued by this object) has run
-      HIP_TRY(hipEventSynchronize(codes_ev));
-      codes_pending = false;
+    CodeStage& c = stage[stage_next];
+    if (c.pending) {  // this pair's previous rewrite (queued by this object, two uploads ago) has run
+      HIP_TRY(hipEventSynchronize(c.ev));
+      c.pending = false;
     }
     HIP_TRY(grid.before_write(s, slots));
-    if (codes_cap < n) {  // grows to the largest world seen (staging is not in use: above)
+    if (c.cap < n) {  // grows to the largest world seen (the pair is not in use: above)
       size_t cap = 1;
       while (cap < n) cap <<= 1;
-      (void)hipHostFree(h_codes);
-      h_codes = nullptr;
-      if (d_codes) HIP_TRY(hipFreeAsync(d_codes, s));
-      d_codes = nullptr;
-      codes_cap = 0;
-      HIP_TRY(hipHostMalloc(&h_codes, cap, hipHostMallocDefault));
-      HIP_TRY(hipMallocAsync((void**)&d_codes, cap, s));
-      codes_cap = cap;
+      (void)hipHostFree(c.h);
+      c.h = nullptr;
+      if (c.d) HIP_TRY(hipFreeAsync(c.d, s));
+      c.d = nullptr;
+      c.cap = 0;
+      HIP_TRY(hipHostMalloc(&c.h, cap, hipHostMallocDefault));
+      HIP_TRY(hipMallocAsync((void**)&c.d, cap, s));
+      c.cap = cap;
     }
-    if (!codes_ev) HIP_TRY(hipEventCreateWithFlags(&codes_ev, hipEventDisableTiming));
+    if (!c.ev) HIP_TRY(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
     const size_t bytes = (size_t)nx << 20;
     if (d_cells_cap < bytes) {  // a fresh grid (stream-ordered on s), all zero
       if (d_cells) HIP_TRY(hipFreeAsync(d_cells, s));
@@ -326,14 +335,15 @@ struct sfrt_voxel {
       box[0] = box[1] = box[2] = 0;
     }
     for (size_t k = 0; k < n; k++)
-      h_codes[k] = blocks[k] == sfrt::kVoxEmpty ? 0 : (uint8_t)(blocks[k] + sfrt::kVoxCellBias);
-    HIP_TRY(hipMemcpyAsync(d_codes, h_codes, n, hipMemcpyHostToDevice, s));
+      c.h[k] = blocks[k] == sfrt::kVoxEmpty ? 0 : (uint8_t)(blocks[k] + sfrt::kVoxCellBias);
+    HIP_TRY(hipMemcpyAsync(c.d, c.h, n, hipMemcpyHostToDevice, s));
     // planes past the new nx are outside the kernel's buffer range, but a later, larger world
     // would see them: the box covers them too while they may hold codes
     const int bx = std::max(nx, box[0]), by = std::max(ny, box[1]), bz = std::max(nz, box[2]);
-    if (sfrt::launch_voxel_cells(d_cells, d_codes, nx, ny, nz, bx, by, bz, s)) return SFRT_E_HIP;
-    HIP_TRY(hipEventRecord(codes_ev, s));
-    codes_pending = true;
+    if (sfrt::launch_voxel_cells(d_cells, c.d, nx, ny, nz, bx, by, bz, s)) return SFRT_E_HIP;
+    HIP_TRY(hipEventRecord(c.ev, s));
+    c.pending = true;
+    stage_next ^= 1;
     HIP_TRY(grid.after_write(s));
     box[0] = nx; box[1] = ny; box[2] = nz;
     blocks_dirty = false;

@@ -508,3 +508,77 @@ def test_voxel_blocks_rewrite_does_not_serialise_other_streams(built, assets):
     finally:
         sphere.close()
         vworld.close()
+
+
+def _aliasing_worlds():
+    """Worlds at the key space's limits (nz = 1024, ny = 1024), where the reference's map key
+    (x << 20) + (y << 10) + z (World.cpp:385) makes a cell past the last column alias the next
+    row's first (z = 1024 is (x, y + 1, 0)) and a cell past the last row the next plane's (y = 1024
+    is (x + 1, 0, z)): rays leaving the world there see those blocks, in the reference and -- as
+    the grid is stored in that key space -- in the kernel."""
+    E = vs.EMPTY
+    out = []
+    # nz = 1024: a floor, and blocks in the first columns z = 0..3 of rows y = 2..5, which the rays
+    # crossing z = 1024 at rows 1..4 meet; the camera near the far end, looking along +z
+    b = np.full((4, 8, 1024), E, dtype=np.int16)
+    b[:, 0, :] = 1
+    b[:, 2:6, 0:4] = 3
+    b[0, :, :] = b[-1, :, :] = 0
+    light = np.zeros(1, dtype=vs.LIGHT_DTYPE)
+    light[0]["pos"], light[0]["intensity"] = (2.0, 3.0, 1020.0), 8.0
+    light[0]["r"] = light[0]["g"] = light[0]["b"] = 1.0
+    light[0]["shadows"] = 1
+    out.append(("z_wraps_to_next_row",
+                vs.VoxelScene(b, np.zeros(0, dtype=vs.DYN_DTYPE), light, (2.5, 2.5, 1019.5), 0.0, 0.1,
+                              view_distance=40.0)))
+    # ny = 1024: blocks on the floor of plane x = 2, which rays of plane x = 1 crossing y = 1024
+    # meet; the camera high up in plane 1, looking up
+    b = np.full((4, 1024, 8), E, dtype=np.int16)
+    b[2, 0, :] = 2
+    b[2, 1, 2:6] = -1
+    b[1, 1020, 0] = 0
+    out.append(("y_wraps_to_next_plane",
+                vs.VoxelScene(b, np.zeros(0, dtype=vs.DYN_DTYPE), np.zeros(0, dtype=vs.LIGHT_DTYPE),
+                              (1.5, 1021.5, 4.5), 0.3, 1.2, view_distance=40.0)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,scene", _aliasing_worlds(), ids=[n for n, _ in _aliasing_worlds()])
+def test_voxel_gpu_key_aliasing_matches_oracle(built, assets, name, scene):
+    """The key space's aliasing (_aliasing_worlds) byte for byte against the restatement, on a
+    world object of its own (these grids are 4 MiB of keys; the rewrite clears them stream-ordered),
+    and the aliasing really shows: the frame differs from the same world with the aliased blocks
+    removed."""
+    import sfrt
+    import torch
+    w, h = 256, 144
+    vw = sfrt.VoxelWorld(0)
+    try:
+        vw.load_assets(assets[0], assets[1], vs.COLORS)
+        frames = []
+        for sc in (scene, None):
+            if sc is None:  # the control: the aliased blocks gone
+                b = scene.blocks.copy()
+                if name.startswith("z_"):
+                    b[:, 2:6, 0:4] = vs.EMPTY
+                else:
+                    b[2, 0, :] = vs.EMPTY
+                    b[2, 1, 2:6] = vs.EMPTY
+                import dataclasses
+                sc = dataclasses.replace(scene, blocks=b)
+            want = oracle.VoxelOracle(sc, w, h, assets[0], assets[1], vs.COLORS).render(host_threads())
+            vw.set_scene(sc, w, h)
+            stream = torch.cuda.Stream()
+            dev = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            vw.render_band(dev.data_ptr(), w * 4, 0, h, stream.cuda_stream)
+            vw.check(stream.cuda_stream)
+            got = dev.cpu().numpy().ravel()
+            g, wv = got.reshape(-1, 4), want.reshape(-1, 4)
+            bad = np.nonzero(np.any(g != wv, axis=1))[0]
+            assert bad.size == 0, (name, f"{bad.size} pixels differ, first ({bad[0] % w}, "
+                                   f"{bad[0] // w}): gpu={g[bad[0]]} oracle={wv[bad[0]]}")
+            frames.append(got)
+        assert not np.array_equal(frames[0], frames[1]), f"{name}: no aliased block in view"
+    finally:
+        vw.close()
