@@ -96,10 +96,16 @@ struct sfrt_glsl {
   // SFRT_OPT_TILE_ORDER (sfrt_glsl_draw): on by default since round 4 (1080p -6 %, 4K -1 %, also
   // with the world moving every frame: profiles/ab/r4_ab9); draw_image stays row-major
   int tile_order_on = 1;
-  sfrt::TileSched sched;               // adaptive tile order (sfrt_sched.h)
+  // adaptive tile order (sfrt_sched.h), one chain per stream: draws on two streams share no order
+  // or cost buffer, so neither waits on the host for the other (as the sphere world, since round 6)
+  sfrt::TileChains scheds;
   // device resources
   hipStream_t stream = nullptr;
   uint32_t* d_mip = nullptr;
+  // set_ground is stream-ordered: the new chain goes up on `stream` behind every draw that read
+  // the old one (through the table slots' events), and draws on other streams wait for it
+  sfrt::SharedBuffer ground;
+  sfrt::PinnedStage mip_stage;
   int mip_levels = 0;
   int mip_w[sfrt::kGlslMipLevels] = {}, mip_h[sfrt::kGlslMipLevels] = {},
       mip_off[sfrt::kGlslMipLevels] = {};
@@ -125,8 +131,10 @@ struct sfrt_glsl {
     sfrt::DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
     (void)hipDeviceSynchronize();
-    sched.release();
+    scheds.release();
     (void)hipFree(d_mip);
+    mip_stage.release();
+    ground.release();
     for (auto& t : slots) t.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
@@ -155,6 +163,7 @@ struct sfrt_glsl {
     if (!d_mip) return SFRT_E_NO_TEXTURE;
     int rc = validate();
     if (rc) return rc;
+    HIP_TRY(ground.before_read(s));  // a set_ground queued on another stream lands first
     std::memset(&f, 0, sizeof f);
     const sfrt_glsl_uniforms& v = u;
     const int sc = v.sphere_count, lc = v.light_count, all = v.all_spheres_count;
@@ -275,15 +284,7 @@ struct sfrt_glsl {
     const size_t bytes = bw + bb + bp + bm;
     sfrt::TableSlot& t = slots[next_slot];
     HIP_TRY(t.reclaim());
-    if (t.cap < bytes) {
-      (void)hipFree(t.d);
-      (void)hipHostFree(t.h);
-      t.d = t.h = nullptr;
-      t.cap = 0;
-      HIP_TRY(hipMalloc(&t.d, bytes));
-      HIP_TRY(hipHostMalloc(&t.h, bytes, hipHostMallocDefault));
-      t.cap = bytes;
-    }
+    HIP_TRY(t.grow(bytes, s));  // no wait on other streams (sfrt_host.h)
     uint8_t* blob = (uint8_t*)t.h;
     std::memcpy(blob, walls.data(), bw);
     std::memcpy(blob + bw, balls.data(), bb);
@@ -383,11 +384,20 @@ int sfrt_glsl_set_ground(sfrt_glsl* g, const uint8_t* rgba, int w, int h) {
   int lw[sfrt::kGlslMipLevels], lh[sfrt::kGlslMipLevels], off[sfrt::kGlslMipLevels], levels = 0;
   build_mips(rgba, w, h, chain, lw, lh, off, &levels);
   sfrt::DeviceGuard dg(g->device);
-  HIP_TRY(hipDeviceSynchronize());  // draws on any stream may still read the old chain
-  (void)hipFree(g->d_mip);
-  g->d_mip = nullptr;
-  HIP_TRY(hipMalloc(&g->d_mip, chain.size() * 4));
-  HIP_TRY(hipMemcpy(g->d_mip, chain.data(), chain.size() * 4, hipMemcpyHostToDevice));
+  // Stream-ordered, no device-wide wait: the new chain goes up on the object's stream behind every
+  // draw that read the old one (device-side waits on the table slots' events, sfrt::SharedBuffer)
+  // and the old chain is freed in that order; draws on other streams wait for the upload.
+  const size_t bytes = chain.size() * 4;
+  void* staged = nullptr;
+  HIP_TRY(g->mip_stage.fill(chain.data(), bytes, &staged));
+  HIP_TRY(g->ground.before_write(g->stream, g->slots));
+  uint32_t* chain_d = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&chain_d, bytes, g->stream));
+  HIP_TRY(hipMemcpyAsync(chain_d, staged, bytes, hipMemcpyHostToDevice, g->stream));
+  HIP_TRY(g->mip_stage.copied(g->stream));
+  if (g->d_mip) HIP_TRY(hipFreeAsync(g->d_mip, g->stream));
+  g->d_mip = chain_d;
+  HIP_TRY(g->ground.after_write(g->stream));
   g->mip_levels = levels;
   for (int k = 0; k < sfrt::kGlslMipLevels; k++) {
     g->mip_w[k] = k < levels ? lw[k] : 0;
@@ -473,14 +483,15 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
   long long tiles = 0;
   const long long key = g->tile_order_on ? sfrt::glsl_tile_key(f, &tiles) : 0;
   sfrt::TileSchedPtrs p;
-  HIP_TRY(g->sched.begin(key, tiles, s, g->tile_order_on, p));
+  sfrt::TileSched& sched = g->scheds.chain[g->scheds.pick(s)];
+  HIP_TRY(sched.begin(key, tiles, s, g->tile_order_on, p));
   f.tile_order = p.tile_order;
   f.tile_cost = p.tile_cost;
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
   f.cost_diff = p.cost_diff ? 1 : 0;
   const bool queued = sfrt::launch_glsl(f, s, g->launch_event()) == 0;
-  HIP_TRY(g->sched.end(p, s, queued));
+  HIP_TRY(sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;
   g->launched(s);
   return SFRT_OK;
@@ -492,11 +503,11 @@ int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
   std::lock_guard<std::mutex> lk(g->mu);
   sfrt::DeviceGuard dg(g->device);
   const size_t px = (size_t)width * height;
-  if (g->d_frame_px < px) {
-    HIP_TRY(hipStreamSynchronize(g->stream));
-    (void)hipFree(g->d_frame);
+  if (g->d_frame_px < px) {  // stream-ordered behind the last draw_image on the object's stream
+    if (g->d_frame) HIP_TRY(hipFreeAsync(g->d_frame, g->stream));
     g->d_frame = nullptr;
-    HIP_TRY(hipMalloc(&g->d_frame, px * 4));
+    g->d_frame_px = 0;
+    HIP_TRY(hipMallocAsync((void**)&g->d_frame, px * 4, g->stream));
     g->d_frame_px = px;
   }
   sfrt::GlslFrame f;

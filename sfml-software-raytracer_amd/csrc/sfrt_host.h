@@ -4,11 +4,35 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstring>
 #include <vector>
 
 #include "sfrt.h"
 
 namespace sfrt {
+
+// hipFree and hipHostFree wait for the whole device: each returned only after 20 ms of work queued
+// on an unrelated stream had drained (tools/gpu/probe_hostalloc.py, profiles/r6u_hip_alloc_calls.txt),
+// while hipMalloc, hipHostMalloc, hipMallocAsync and hipFreeAsync did not.  So buffers that grow
+// while frames run -- per-frame tables, staging, device frames -- are stream-ordered device memory
+// (hipMallocAsync / hipFreeAsync behind the waits that make the old buffer idle), and a replaced
+// pinned host buffer is retired until its owner is destroyed (capacities grow geometrically, so the
+// retired bytes stay below the live ones).
+struct RetiredHost {
+  std::vector<void*> bufs;
+  void add(void* h) {
+    if (h) bufs.push_back(h);
+  }
+  void release() {
+    for (void* h : bufs) (void)hipHostFree(h);
+    bufs.clear();
+  }
+};
+inline size_t grown_capacity(size_t cap, size_t need) {
+  size_t c = cap > 256 ? cap : 256;
+  while (c < need) c += c / 2;
+  return c;
+}
 
 // Makes `dev` the calling thread's current HIP device for the guard's scope and
 // restores the caller's device afterwards (a C-ABI call must not move it).
@@ -57,6 +81,23 @@ struct TableSlot {
   }
   // After queuing a launch on s that reads the slot (use_on(s) came first).
   hipError_t launched(hipStream_t s) { return mark(s); }
+  // Room for `bytes` (after reclaim(): every earlier user has finished), waiting for no other
+  // stream: the device tables reallocated in the order of s, the staging stream; the old pinned
+  // copy retired (RetiredHost).
+  hipError_t grow(size_t bytes, hipStream_t s) {
+    if (cap >= bytes) return hipSuccess;
+    const size_t c = grown_capacity(cap, bytes);
+    hipError_t e;
+    if (d && (e = hipFreeAsync(d, s)) != hipSuccess) return e;
+    d = nullptr;
+    retired.add(h);
+    h = nullptr;
+    cap = 0;
+    if ((e = hipMallocAsync(&d, c, s)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&h, c, hipHostMallocDefault)) != hipSuccess) return e;
+    cap = c;
+    return hipSuccess;
+  }
   // The same through the launch itself: the event to pass to the kernel launch as its stop event
   // (hipExtLaunchKernelGGL: the dispatch packet's own completion signal records it, so no marker
   // packet sits between two frames -- a hipEventRecord after every launch cost the 1080p voxel
@@ -69,6 +110,7 @@ struct TableSlot {
   void release() {
     (void)hipFree(d);
     (void)hipHostFree(h);
+    retired.release();
     if (ev) (void)hipEventDestroy(ev);
     d = h = nullptr;
     ev = nullptr;
@@ -77,6 +119,7 @@ struct TableSlot {
   }
 
  private:
+  RetiredHost retired;
   hipError_t mark(hipStream_t s) {
     const hipError_t e = hipEventRecord(ev, s);
     if (e != hipSuccess) return e;
@@ -143,6 +186,55 @@ struct SharedBuffer {
     have_written = false;
     current.clear();
   }
+};
+
+// Pinned staging for a stream-ordered upload from the caller's (pageable) memory: the bytes are
+// copied into the staging buffer on the host, then to the device on a stream; the buffer is reused
+// only after its last device copy has run (a host wait on that copy alone, never on the device).
+struct PinnedStage {
+  void* h = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+
+  // The staging buffer holding a copy of src[0, bytes).
+  hipError_t fill(const void* src, size_t bytes, void** out) {
+    hipError_t e;
+    if (pending) {
+      if ((e = hipEventSynchronize(ev)) != hipSuccess) return e;
+      pending = false;
+    }
+    if (cap < bytes) {  // the old buffer retired, not freed (RetiredHost)
+      const size_t c = grown_capacity(cap, bytes);
+      retired.add(h);
+      h = nullptr;
+      cap = 0;
+      if ((e = hipHostMalloc(&h, c, hipHostMallocDefault)) != hipSuccess) return e;
+      cap = c;
+    }
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    std::memcpy(h, src, bytes);
+    *out = h;
+    return hipSuccess;
+  }
+  // After the device copy from the staging buffer was queued on s.
+  hipError_t copied(hipStream_t s) {
+    const hipError_t e = hipEventRecord(ev, s);
+    if (e == hipSuccess) pending = true;
+    return e;
+  }
+  void release() {
+    (void)hipHostFree(h);
+    retired.release();
+    if (ev) (void)hipEventDestroy(ev);
+    h = nullptr;
+    ev = nullptr;
+    cap = 0;
+    pending = false;
+  }
+
+ private:
+  RetiredHost retired;
 };
 
 }  // namespace sfrt

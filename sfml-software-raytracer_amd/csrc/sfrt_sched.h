@@ -70,13 +70,24 @@ struct TileSched {
     if (key == 0 || mode == 0 || tiles >= kOrderMaxTiles) return hipSuccess;
     hipError_t e;
     if (tiles > cap) {  // (re)allocate; a new chain starts
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
-      release();
+      // Stream-ordered, no device-wide wait (a hipDeviceSynchronize here had made the first draw
+      // on a new stream wait for every other stream's work): the old buffers are freed in the order
+      // of the stream of their last launch, the new ones allocated in the order of s, the stream
+      // of the launch that will use them first.
+      const hipStream_t fs = have_last ? last_stream : s;
+      for (int q = 0; q < 2; q++) {
+        if (order[q] && (e = hipFreeAsync(order[q], fs)) != hipSuccess) return e;
+        if (cost[q] && (e = hipFreeAsync(cost[q], fs)) != hipSuccess) return e;
+        order[q] = nullptr;
+        cost[q] = nullptr;
+      }
+      cap = 0;
       reset();
       for (int q = 0; q < 2; q++) {
-        if ((e = hipMalloc(&order[q], sizeof(uint32_t) * (size_t)order_capacity(tiles))) != hipSuccess)
+        if ((e = hipMallocAsync((void**)&order[q], sizeof(uint32_t) * (size_t)order_capacity(tiles),
+                                s)) != hipSuccess)
           return e;
-        if ((e = hipMalloc(&cost[q], (size_t)tiles)) != hipSuccess) return e;
+        if ((e = hipMallocAsync((void**)&cost[q], (size_t)tiles, s)) != hipSuccess) return e;
       }
       cap = tiles;
     }

@@ -95,19 +95,6 @@ struct DevTex {
   size_t cap = 0;
 };
 
-int upload_texture(DevTex& t, const uint8_t* rgba, int w, int h) {
-  const size_t n = (size_t)w * h;
-  if (t.cap < n) {
-    (void)hipFree(t.d);
-    t.d = nullptr;
-    HIP_TRY(hipMalloc(&t.d, n * 4));
-    t.cap = n;
-  }
-  HIP_TRY(hipMemcpy(t.d, rgba, n * 4, hipMemcpyHostToDevice));
-  t.w = w;
-  t.h = h;
-  return SFRT_OK;
-}
 
 }  // namespace
 
@@ -144,7 +131,10 @@ struct sfrt_voxel {
   };
   CodeStage stage[2];
   int stage_next = 0;
-  sfrt::SharedBuffer grid;   // d_cells' rewrites ordered against its readers (sfrt_host.h)
+  sfrt::RetiredHost retired_host;  // replaced pinned buffers (sfrt_host.h: hipHostFree waits for all)
+  // d_cells' and the textures' rewrites ordered against their readers (sfrt_host.h)
+  sfrt::SharedBuffer shared;
+  sfrt::PinnedStage tex_stage;  // texture uploads from the caller's memory
   // Per-frame tables (columns | rows | dyn | lights) in a ring of slots, each
   // with pinned staging and the event of the last launch that read it, so
   // launches on different streams never see a table overwritten under them.
@@ -163,14 +153,14 @@ struct sfrt_voxel {
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
   int tile_order_on = 0;     // SFRT_OPT_TILE_ORDER: off by default here (slower)
-  sfrt::TileSched sched;     // adaptive tile order (sfrt_sched.h), render_band
+  sfrt::TileChains scheds;   // adaptive tile order (sfrt_sched.h), render_band; one chain per stream
   std::mutex mu;
 
   ~sfrt_voxel() {
     sfrt::DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
     (void)hipDeviceSynchronize();
-    sched.release();
+    scheds.release();
     for (auto& t : tex) (void)hipFree(t.d);
     for (auto& t : dyn_tex) (void)hipFree(t.d);
     (void)hipDeviceSynchronize();
@@ -180,7 +170,9 @@ struct sfrt_voxel {
       (void)hipHostFree(c.h);
       if (c.ev) (void)hipEventDestroy(c.ev);
     }
-    grid.release();
+    retired_host.release();
+    shared.release();
+    tex_stage.release();
     for (auto& t : slots) t.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
@@ -208,7 +200,7 @@ struct sfrt_voxel {
       sfrt::TableSlot& t = slots[cur_slot];  // still holds this scene's tables; launched() re-marks it
       const int rc = blocks_upload(s);  // first: fill_frame reads d_cells
       if (rc != SFRT_OK) return rc;
-      HIP_TRY(grid.before_read(s));
+      HIP_TRY(shared.before_read(s));
       HIP_TRY(t.use_on(s));  // staged, or last read, on another stream: wait for it
       fill_frame(f, (uint8_t*)t.d, staged_off);
       return SFRT_OK;
@@ -263,15 +255,7 @@ struct sfrt_voxel {
     const size_t bytes = b_col + b_row + b_dyn + b_lit + 16;
     sfrt::TableSlot& t = slots[next_slot];
     HIP_TRY(t.reclaim());
-    if (t.cap < bytes) {
-      (void)hipFree(t.d);
-      (void)hipHostFree(t.h);
-      t.d = t.h = nullptr;
-      t.cap = 0;
-      HIP_TRY(hipMalloc(&t.d, bytes));
-      HIP_TRY(hipHostMalloc(&t.h, bytes, hipHostMallocDefault));
-      t.cap = bytes;
-    }
+    HIP_TRY(t.grow(bytes, s));  // no wait on other streams (sfrt_host.h)
     uint8_t* h = (uint8_t*)t.h;
     std::memcpy(h, col.data(), col.size() * sizeof(float));
     std::memcpy(h + b_col, row.data(), row.size() * sizeof(float));
@@ -289,7 +273,7 @@ struct sfrt_voxel {
     staged_off[2] = b_col + b_row + b_dyn;
     const int rc = blocks_upload(s);  // first: fill_frame reads d_cells
     if (rc != SFRT_OK) return rc;
-    HIP_TRY(grid.before_read(s));
+    HIP_TRY(shared.before_read(s));
     fill_frame(f, (uint8_t*)t.d, staged_off);
     return SFRT_OK;
   }
@@ -310,11 +294,11 @@ struct sfrt_voxel {
       HIP_TRY(hipEventSynchronize(c.ev));
       c.pending = false;
     }
-    HIP_TRY(grid.before_write(s, slots));
+    HIP_TRY(shared.before_write(s, slots));
     if (c.cap < n) {  // grows to the largest world seen (the pair is not in use: above)
       size_t cap = 1;
       while (cap < n) cap <<= 1;
-      (void)hipHostFree(c.h);
+      retired_host.add(c.h);  // not hipHostFree: it would wait for the whole device
       c.h = nullptr;
       if (c.d) HIP_TRY(hipFreeAsync(c.d, s));
       c.d = nullptr;
@@ -344,9 +328,33 @@ struct sfrt_voxel {
     HIP_TRY(hipEventRecord(c.ev, s));
     c.pending = true;
     stage_next ^= 1;
-    HIP_TRY(grid.after_write(s));
+    HIP_TRY(shared.after_write(s));
     box[0] = nx; box[1] = ny; box[2] = nz;
     blocks_dirty = false;
+    return SFRT_OK;
+  }
+
+  // A texture (textures[slot] or dynTextures[slot], World.h:90-91) uploaded stream-ordered, like the
+  // grid: on the object's stream behind every frame that read the old texels (SharedBuffer), a
+  // larger one in a new buffer with the old one freed in that order.  Frames queued after the call
+  // read the new texels; nothing waits for the device.
+  int upload_texture(DevTex& t, const uint8_t* rgba, int w, int h) {
+    const size_t n = (size_t)w * h;
+    void* staged = nullptr;
+    HIP_TRY(tex_stage.fill(rgba, n * 4, &staged));
+    HIP_TRY(shared.before_write(stream, slots));
+    if (t.cap < n) {
+      uint32_t* d = nullptr;
+      HIP_TRY(hipMallocAsync((void**)&d, n * 4, stream));
+      if (t.d) HIP_TRY(hipFreeAsync(t.d, stream));
+      t.d = d;
+      t.cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(t.d, staged, n * 4, hipMemcpyHostToDevice, stream));
+    HIP_TRY(tex_stage.copied(stream));
+    HIP_TRY(shared.after_write(stream));
+    t.w = w;
+    t.h = h;
     return SFRT_OK;
   }
 
@@ -462,16 +470,14 @@ int sfrt_voxel_load_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w,
   if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   sfrt::DeviceGuard g(v->device);
-  HIP_TRY(hipDeviceSynchronize());  // launches on any stream may read it
-  return upload_texture(v->tex[slot], rgba, w, h);
+  return v->upload_texture(v->tex[slot], rgba, w, h);
 }
 
 int sfrt_voxel_load_dyn_texture(sfrt_voxel* v, int slot, const uint8_t* rgba, int w, int h) {
   if (!v || !rgba || slot < 0 || slot >= sfrt::kVoxSlots || w <= 0 || h <= 0) return SFRT_E_INVALID;
   std::lock_guard<std::mutex> lk(v->mu);
   sfrt::DeviceGuard g(v->device);
-  HIP_TRY(hipDeviceSynchronize());
-  return upload_texture(v->dyn_tex[slot], rgba, w, h);
+  return v->upload_texture(v->dyn_tex[slot], rgba, w, h);
 }
 
 int sfrt_voxel_set_colors(sfrt_voxel* v, const uint8_t* rgba, int count) {
@@ -511,10 +517,11 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   if (sub_w == 0 || sub_h == 0) return SFRT_OK;
   sfrt::DeviceGuard g(v->device);
   const size_t px = (size_t)sub_w * sub_h;
-  if (v->d_frame_px < px) {
-    (void)hipFree(v->d_frame);
+  if (v->d_frame_px < px) {  // the last update_image finished with it (it waits for its copy)
+    if (v->d_frame) HIP_TRY(hipFreeAsync(v->d_frame, v->stream));
     v->d_frame = nullptr;
-    HIP_TRY(hipMalloc(&v->d_frame, px * 4));
+    v->d_frame_px = 0;
+    HIP_TRY(hipMallocAsync((void**)&v->d_frame, px * 4, v->stream));
     v->d_frame_px = px;
   }
   sfrt::VoxFrame f;
@@ -561,14 +568,15 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   long long tiles = 0;
   const long long key = v->tile_order_on ? sfrt::voxel_tile_key(f, &tiles) : 0;
   sfrt::TileSchedPtrs p;
-  HIP_TRY(v->sched.begin(key, tiles, s, v->tile_order_on, p));
+  sfrt::TileSched& sched = v->scheds.chain[v->scheds.pick(s)];
+  HIP_TRY(sched.begin(key, tiles, s, v->tile_order_on, p));
   f.tile_order = p.tile_order;
   f.tile_cost = p.tile_cost;
   f.prev_cost = p.prev_cost;
   f.next_order = p.next_order;
   f.cost_diff = p.cost_diff ? 1 : 0;
   const bool queued = sfrt::launch_voxel(f, s, v->launch_event()) == 0;
-  HIP_TRY(v->sched.end(p, s, queued));
+  HIP_TRY(sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;
   v->launched(s);
   return SFRT_OK;

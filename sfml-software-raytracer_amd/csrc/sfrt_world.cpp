@@ -150,6 +150,8 @@ struct sfrt_world {
   size_t d_frame_px = 0;
   uint32_t* h_stage = nullptr;  // pinned D2H staging
   size_t h_stage_px = 0;
+  sfrt::RetiredHost retired_host;  // replaced pinned buffers (sfrt_host.h)
+  std::vector<void*> retired_device;  // replaced record rings, freed with the world
   // --- frame pipeline (display path): render k+1 while frame k is copied ---
   struct PipeSlot {
     uint32_t* d_buf = nullptr;
@@ -189,6 +191,8 @@ struct sfrt_world {
     }
     (void)hipFree(d_frame);
     (void)hipHostFree(h_stage);
+    retired_host.release();
+    for (void* p : retired_device) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -277,24 +281,28 @@ struct sfrt_world {
     }
   }
 
+  // A larger record ring, waiting for no stream (sfrt_host.h: hipFree / hipHostFree would wait for
+  // the whole device): launches queued on any stream may still read the old slots, so the old
+  // buffers are retired until the world is destroyed (the ring grows geometrically, and only past
+  // the largest sphere count seen); the new ones are plain allocations every stream may use.
   int ensure_sphere_buffers(int n) {
     if (n <= d_spheres_cap) return SFRT_OK;
-    HIP_TRY(hipDeviceSynchronize());  // launches on any stream may read the old slots
+    const int cap = (int)sfrt::grown_capacity((size_t)d_spheres_cap, (size_t)n);
     for (int k = 0; k < kRing; k++) {
-      (void)hipFree(d_spheres[k]);
-      (void)hipHostFree(h_spheres[k]);
+      if (d_spheres[k]) retired_device.push_back(d_spheres[k]);
+      retired_host.add(h_spheres[k]);
       d_spheres[k] = nullptr;
       h_spheres[k] = nullptr;
       spheres_pending[k] = false;
     }
     d_spheres_cap = 0;
     for (int k = 0; k < kRing; k++) {
-      HIP_TRY(hipMalloc(&d_spheres[k], sizeof(sfrt::SphereRec) * (size_t)n));
-      HIP_TRY(hipHostMalloc(&h_spheres[k], sizeof(sfrt::SphereRec) * (size_t)n,
+      HIP_TRY(hipMalloc(&d_spheres[k], sizeof(sfrt::SphereRec) * (size_t)cap));
+      HIP_TRY(hipHostMalloc(&h_spheres[k], sizeof(sfrt::SphereRec) * (size_t)cap,
                             hipHostMallocDefault));
       if (!spheres_ev[k]) HIP_TRY(hipEventCreateWithFlags(&spheres_ev[k], hipEventDisableTiming));
     }
-    d_spheres_cap = n;
+    d_spheres_cap = cap;
     return SFRT_OK;
   }
 
@@ -681,15 +689,20 @@ int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart, int yadd
   if (sub_w == 0 || sub_h == 0) return SFRT_OK;
   sfrt::DeviceGuard g(w->device);
   const size_t px = (size_t)sub_w * sub_h;
+  // Growth waits for no other stream (sfrt_host.h: hipFree / hipHostFree wait for the whole
+  // device): the device frame stream-ordered on the world's stream, behind the last update_image
+  // (which waited for its own copy); the old pinned staging retired.
   if (w->d_frame_px < px) {
-    (void)hipFree(w->d_frame);
+    if (w->d_frame) HIP_TRY(hipFreeAsync(w->d_frame, w->stream));
     w->d_frame = nullptr;
-    HIP_TRY(hipMalloc(&w->d_frame, px * 4));
+    w->d_frame_px = 0;
+    HIP_TRY(hipMallocAsync((void**)&w->d_frame, px * 4, w->stream));
     w->d_frame_px = px;
   }
   if (w->h_stage_px < px) {
-    (void)hipHostFree(w->h_stage);
+    w->retired_host.add(w->h_stage);
     w->h_stage = nullptr;
+    w->h_stage_px = 0;
     HIP_TRY(hipHostMalloc(&w->h_stage, px * 4, hipHostMallocDefault));
     w->h_stage_px = px;
   }
@@ -880,11 +893,12 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
     HIP_TRY(hipHostMalloc(&slot.h_status, sizeof(int), hipHostMallocDefault));
   }
   const size_t px = (size_t)w->width * w->height;
-  if (slot.px < px) {
-    if (slot.used) HIP_TRY(hipEventSynchronize(slot.copied));  // its last copy still reads d_buf
-    (void)hipFree(slot.d_buf);
+  if (slot.px < px) {  // stream-ordered: freed behind its last copy, no device-wide wait
+    if (slot.used) HIP_TRY(hipStreamWaitEvent(w->stream, slot.copied, 0));
+    if (slot.d_buf) HIP_TRY(hipFreeAsync(slot.d_buf, w->stream));
     slot.d_buf = nullptr;
-    HIP_TRY(hipMalloc(&slot.d_buf, px * 4));
+    slot.px = 0;
+    HIP_TRY(hipMallocAsync(&slot.d_buf, px * 4, w->stream));
     slot.px = px;
   }
   // The slot's previous frame must have left d_buf before this render writes it.

@@ -468,6 +468,12 @@ class VoxelWorld:
         col = np.ascontiguousarray(colors, dtype=np.uint8)
         _check(lib().sfrt_voxel_set_colors(self._h, col.ctypes.data, col.shape[0]), "set_colors")
 
+    def load_texture(self, slot: int, rgba, w: int, h: int) -> None:
+        """textures[slot] (World.h:90) alone: sfrt_voxel_load_texture, stream-ordered."""
+        buf = np.ascontiguousarray(rgba, dtype=np.uint8)
+        _check(lib().sfrt_voxel_load_texture(self._h, int(slot), buf.ctypes.data, int(w), int(h)),
+               "load_texture")
+
     def set_scene(self, scene, width: int, height: int) -> None:
         self.width, self.height = int(width), int(height)
         _check(lib().sfrt_voxel_set_size(self._h, self.width, self.height), "set_size")

@@ -516,3 +516,51 @@ def test_gpu_tables_restaged_after_every_uniform_setter(shader, floor):
     assert np.array_equal(got, want(u3)), first_diff(got, want(u3), w)
     shader.set_uniforms(u)                                     # the block again
     assert np.array_equal(frame(), first)
+
+
+@pytest.mark.gpu
+def test_gpu_ground_change_is_stream_ordered(built, floor):
+    """sfrt_glsl_set_ground without a device-wide wait (sfrt_glsl.cpp, sfrt::SharedBuffer): a draw
+    on stream B queued behind ~20 ms of work still reads the ground it was queued with when a new
+    ground is set right after (the upload waits, on the device, for that draw); the call and the
+    draw on A return while B's queue is still busy; each frame equals the restatement with its own
+    ground.  Then a larger ground (a new buffer) and back.  The draw on A
+    does not wait on the host for B's either: each stream has its own tile-order chain
+    (sfrt_sched.h TileChains, since round 6 also for the GLSL and voxel renderers)."""
+    import sfrt
+    import torch
+    w, h = 320, 180
+    u = gs.default_uniforms(w, h, 0.4, 0.1, frames=7)
+    grounds = [floor, synthetic_ground(), synthetic_ground(128, 256, seed=9), floor]
+    s = sfrt.GlslShader(0)
+    try:
+        s.set_ground(*grounds[0])
+        s.set_uniforms(u)
+        a, b = torch.cuda.Stream(), torch.cuda.Stream()
+        warm = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
+        s.draw(warm.data_ptr(), w, h, w * 4, 0, h, a.cuda_stream)
+        torch.cuda.synchronize()
+        frames = []
+        for k in range(1, len(grounds)):
+            old = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            with torch.cuda.stream(b):
+                torch.cuda._sleep(40_000_000)
+            s.draw(old.data_ptr(), w, h, w * 4, 0, h, b.cuda_stream)   # reads grounds[k - 1]
+            new = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            assert not b.query(), "B drained before the calls (the test's own setup waited)"
+            s.set_ground(*grounds[k])
+            busy = {"set_ground": not b.query()}
+            s.draw(new.data_ptr(), w, h, w * 4, 0, h, a.cuda_stream)   # reads grounds[k]
+            busy["draw on A"] = not b.query()
+            frames.append((grounds[k - 1], old, grounds[k], new, busy))
+            torch.cuda.synchronize()
+        s.check(a.cuda_stream)
+        s.check(b.cuda_stream)
+        for g_old, old, g_new, new, busy in frames:
+            assert all(busy.values()), f"waited for the queued draw on B: {busy}"
+            for g, buf in ((g_old, old), (g_new, new)):
+                want = oracle.GlslOracle(u, *g).render(w, h, host_threads())
+                got = buf.cpu().numpy().ravel()
+                assert np.array_equal(got, want), first_diff(got, want, w)
+    finally:
+        s.close()

@@ -134,3 +134,95 @@ def test_sphere_tile_order_chains_more_streams_than_chains(built, floor):
     for i in range(k):
         got = bufs[i].cpu().numpy().ravel()
         assert np.array_equal(got, want[i]), f"frame {i}: {_report(got, want[i], w)}"
+
+
+@pytest.mark.gpu
+def test_growth_waits_for_no_other_stream(built, floor):
+    """Buffers that grow between frames -- the sphere world's record ring (more spheres) and
+    host-frame staging (a larger update_image), the voxel renderer's per-frame tables (a larger
+    frame), the GLSL renderer's tables (more balls), the tile-order buffers of a new stream's
+    chain, the pipelined display slots -- are reallocated without waiting for unrelated work:
+    hipFree / hipHostFree wait for the whole device, so these paths use stream-ordered device
+    memory and retire replaced pinned buffers (sfrt_host.h).  With ~20 ms of work queued on an
+    unrelated stream, every call returns while that work is still pending, and the frames equal
+    the same frames rendered on their own afterwards."""
+    import sfrt
+    import torch
+    busy_stream = torch.cuda.Stream()
+    s1 = torch.cuda.Stream()
+
+    def hold():
+        torch.cuda.synchronize()
+        with torch.cuda.stream(busy_stream):
+            torch.cuda._sleep(40_000_000)
+
+    def still_busy(what):
+        assert not busy_stream.query(), f"{what} waited for an unrelated stream"
+
+    checks = []
+    with sfrt.World(0) as world:
+        world.load_texture(*floor)
+        world.set_scene(scenes.default10(), 320, 240)
+        small = np.zeros(320 * 240 * 4, np.uint8)
+        world.update_image(small)
+        # the record ring grows (65 -> 300 spheres) and a new stream's chain is allocated
+        sc = scenes.Scene("lcg300", scenes.sort_spheres(scenes.lcg_spheres(299, 77)))
+        hold()
+        world.set_scene(sc, 640, 360)
+        dev = torch.empty((360, 640 * 4), dtype=torch.uint8, device="cuda:0")
+        world.render_band(dev.data_ptr(), 640 * 4, 0, 360, s1.cuda_stream)
+        still_busy("sphere record ring growth / new chain")
+        checks.append(("sphere ring", dev, sc, 640, 360))
+        # host-frame staging grows (update_image is synchronous on the world's own stream only)
+        hold()
+        big = np.zeros(640 * 360 * 4, np.uint8)
+        world.update_image(big)
+        still_busy("update_image staging growth")
+        torch.cuda.synchronize()
+        ref = np.zeros_like(big)
+        world.update_image(ref)
+        assert np.array_equal(big, ref)
+        for name, buf, scx, w, h in checks:
+            torch.cuda.synchronize()
+            want = np.zeros(w * h * 4, np.uint8)
+            world.set_scene(scx, w, h)
+            world.update_image(want)
+            assert np.array_equal(buf.cpu().numpy().ravel(), want), name
+    # voxel tables grow with the frame
+    vw = sfrt.VoxelWorld(0)
+    try:
+        tex, dyn = vs.load_textures()
+        vw.load_assets(tex, dyn, vs.COLORS)
+        scene = vs.default_world((20.5, 2.2, 40.5), 1.0, 0.1)
+        vw.set_scene(scene, 160, 90)
+        warm = torch.empty((90, 160 * 4), dtype=torch.uint8, device="cuda:0")
+        vw.render_band(warm.data_ptr(), 160 * 4, 0, 90, s1.cuda_stream)
+        hold()
+        vw.set_scene(scene, 800, 450)
+        vdev = torch.empty((450, 800 * 4), dtype=torch.uint8, device="cuda:0")
+        vw.render_band(vdev.data_ptr(), 800 * 4, 0, 450, s1.cuda_stream)
+        still_busy("voxel table growth")
+        torch.cuda.synchronize()
+        assert np.array_equal(vdev.cpu().numpy().ravel(), vw.render())
+    finally:
+        vw.close()
+    # GLSL tables grow with the ball count
+    g = sfrt.GlslShader(0)
+    try:
+        g.set_ground(*floor)
+        u0 = gs.random_uniforms(2, 4, 1, 3, 320, 180)
+        g.set_uniforms(u0)
+        gw = torch.empty((180, 320 * 4), dtype=torch.uint8, device="cuda:0")
+        g.draw(gw.data_ptr(), 320, 180, 320 * 4, 0, 180, s1.cuda_stream)
+        hold()
+        u1 = gs.random_uniforms(3, 40, 4, 50, 320, 180)
+        g.set_uniforms(u1)
+        g.draw(gw.data_ptr(), 320, 180, 320 * 4, 0, 180, s1.cuda_stream)
+        still_busy("GLSL table growth")
+        torch.cuda.synchronize()
+        again = torch.empty_like(gw)
+        g.draw(again.data_ptr(), 320, 180, 320 * 4, 0, 180, s1.cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(gw, again)
+    finally:
+        g.close()

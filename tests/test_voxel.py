@@ -582,3 +582,52 @@ def test_voxel_gpu_key_aliasing_matches_oracle(built, assets, name, scene):
         assert not np.array_equal(frames[0], frames[1]), f"{name}: no aliased block in view"
     finally:
         vw.close()
+
+
+@pytest.mark.gpu
+def test_voxel_texture_upload_is_stream_ordered(built, assets):
+    """sfrt_voxel_load_texture without a device-wide wait (sfrt_voxel.cpp upload_texture,
+    sfrt::SharedBuffer): a frame on stream B queued behind ~20 ms of work still reads the texture
+    it was queued with when textures[0] is replaced right after; the call returns while B is busy;
+    both frames equal the restatement with their own texture set, also for a larger texture (a new
+    buffer)."""
+    import sfrt
+    import torch
+    w, h = 320, 180
+    case = (w, h, (20.5, 2.2, 40.5), 1.0, 0.1)
+    scene, _ = voxel_oracle(case, assets)
+    rng = np.random.default_rng(3)
+    tex0 = list(assets[0])
+    alt = [(rng.integers(0, 256, t[1] * t[2] * 4, dtype=np.uint8), t[1], t[2]) for t in tex0[:1]]
+    big = (rng.integers(0, 256, 128 * 128 * 4, dtype=np.uint8), 128, 128)
+    sets = [tex0, [alt[0]] + tex0[1:], [big] + tex0[1:], tex0]
+    vw = sfrt.VoxelWorld(0)
+    try:
+        vw.load_assets(sets[0], assets[1], vs.COLORS)
+        vw.set_scene(scene, w, h)
+        a, b = torch.cuda.Stream(), torch.cuda.Stream()
+        warm = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
+        vw.render_band(warm.data_ptr(), w * 4, 0, h, a.cuda_stream)
+        torch.cuda.synchronize()
+        frames = []
+        for k in range(1, len(sets)):
+            old = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            with torch.cuda.stream(b):
+                torch.cuda._sleep(40_000_000)
+            vw.render_band(old.data_ptr(), w * 4, 0, h, b.cuda_stream)    # reads sets[k - 1]
+            rgba, tw, th = sets[k][0]
+            vw.load_texture(0, rgba, tw, th)
+            busy = not b.query()
+            new = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            vw.render_band(new.data_ptr(), w * 4, 0, h, a.cuda_stream)    # reads sets[k]
+            frames.append((sets[k - 1], old, sets[k], new, busy))
+            torch.cuda.synchronize()
+        vw.check(a.cuda_stream)
+        vw.check(b.cuda_stream)
+        for t_old, old, t_new, new, busy in frames:
+            assert busy, "load_texture waited for the queued frame on B"
+            for t, buf in ((t_old, old), (t_new, new)):
+                want = oracle.VoxelOracle(scene, w, h, t, assets[1], vs.COLORS).render(host_threads())
+                assert np.array_equal(buf.cpu().numpy().ravel(), want)
+    finally:
+        vw.close()
