@@ -465,7 +465,7 @@ def test_gpu_tables_reused_across_streams(shader, floor):
         bb = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
         torch.cuda.synchronize()
         with torch.cuda.stream(a):
-            torch.cuda._sleep(40_000_000)  # ~20 ms of queued work ahead of A's staging copy
+            torch.cuda._sleep(100_000_000)  # ~50 ms of queued work ahead of A's staging copy
         shader.draw(ba.data_ptr(), w, h, w * 4, 0, h, a.cuda_stream)   # stages on A
         shader.draw(bb.data_ptr(), w, h, w * 4, 0, h, b.cuda_stream)   # reuses on B at once
         outs.append((u, ba, bb))
@@ -521,7 +521,7 @@ def test_gpu_tables_restaged_after_every_uniform_setter(shader, floor):
 @pytest.mark.gpu
 def test_gpu_ground_change_is_stream_ordered(built, floor):
     """sfrt_glsl_set_ground without a device-wide wait (sfrt_glsl.cpp, sfrt::SharedBuffer): a draw
-    on stream B queued behind ~20 ms of work still reads the ground it was queued with when a new
+    on stream B queued behind ~50 ms of work still reads the ground it was queued with when a new
     ground is set right after (the upload waits, on the device, for that draw); the call and the
     draw on A return while B's queue is still busy; each frame equals the restatement with its own
     ground.  Then a larger ground (a new buffer) and back.  The draw on A
@@ -544,7 +544,7 @@ def test_gpu_ground_change_is_stream_ordered(built, floor):
         for k in range(1, len(grounds)):
             old = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
             with torch.cuda.stream(b):
-                torch.cuda._sleep(40_000_000)
+                torch.cuda._sleep(100_000_000)
             s.draw(old.data_ptr(), w, h, w * 4, 0, h, b.cuda_stream)   # reads grounds[k - 1]
             new = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
             assert not b.query(), "B drained before the calls (the test's own setup waited)"

@@ -143,7 +143,7 @@ def test_growth_waits_for_no_other_stream(built, floor):
     frame), the GLSL renderer's tables (more balls), the tile-order buffers of a new stream's
     chain, the pipelined display slots -- are reallocated without waiting for unrelated work:
     hipFree / hipHostFree wait for the whole device, so these paths use stream-ordered device
-    memory and retire replaced pinned buffers (sfrt_host.h).  With ~20 ms of work queued on an
+    memory and retire replaced pinned buffers (sfrt_host.h).  With ~50 ms of work queued on an
     unrelated stream, every call returns while that work is still pending, and the frames equal
     the same frames rendered on their own afterwards."""
     import sfrt
@@ -154,7 +154,7 @@ def test_growth_waits_for_no_other_stream(built, floor):
     def hold():
         torch.cuda.synchronize()
         with torch.cuda.stream(busy_stream):
-            torch.cuda._sleep(40_000_000)
+            torch.cuda._sleep(100_000_000)
 
     def still_busy(what):
         assert not busy_stream.query(), f"{what} waited for an unrelated stream"

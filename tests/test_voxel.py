@@ -175,7 +175,7 @@ def test_voxel_tables_reused_across_streams(vworld, assets):
         bb = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
         torch.cuda.synchronize()
         with torch.cuda.stream(a):
-            torch.cuda._sleep(40_000_000)  # ~20 ms of queued work ahead of A's staging copy
+            torch.cuda._sleep(100_000_000)  # ~50 ms of queued work ahead of A's staging copy
         vworld.render_band(ba.data_ptr(), w * 4, 0, h, a.cuda_stream)   # stages on A
         vworld.render_band(bb.data_ptr(), w * 4, 0, h, b.cuda_stream)   # reuses on B at once
         scenes_.append((sc, ba, bb))
@@ -587,7 +587,7 @@ def test_voxel_gpu_key_aliasing_matches_oracle(built, assets, name, scene):
 @pytest.mark.gpu
 def test_voxel_texture_upload_is_stream_ordered(built, assets):
     """sfrt_voxel_load_texture without a device-wide wait (sfrt_voxel.cpp upload_texture,
-    sfrt::SharedBuffer): a frame on stream B queued behind ~20 ms of work still reads the texture
+    sfrt::SharedBuffer): a frame on stream B queued behind ~50 ms of work still reads the texture
     it was queued with when textures[0] is replaced right after; the call returns while B is busy;
     both frames equal the restatement with their own texture set, also for a larger texture (a new
     buffer)."""
@@ -613,7 +613,7 @@ def test_voxel_texture_upload_is_stream_ordered(built, assets):
         for k in range(1, len(sets)):
             old = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
             with torch.cuda.stream(b):
-                torch.cuda._sleep(40_000_000)
+                torch.cuda._sleep(100_000_000)
             vw.render_band(old.data_ptr(), w * 4, 0, h, b.cuda_stream)    # reads sets[k - 1]
             rgba, tw, th = sets[k][0]
             vw.load_texture(0, rgba, tw, th)
