@@ -7,7 +7,7 @@
 // its per-tile march-step classes into cost[k % 2], and -- from its extra
 // workgroup 0 -- sorts cost[(k+1) % 2] (launch k-1's) into order[(k+1) % 2].
 // Consecutive launches are ordered by their stream; before a launch on another
-// stream than the previous one, the host waits for the previous one.  An order is
+// stream than the previous one, the host waits for the device (below).  An order is
 // used only when the two launches before had the same grid (key).  Scheduling
 // only: every tile is rendered once whatever the order.
 #pragma once
@@ -69,15 +69,22 @@ struct TileSched {
     pending_key = 0;
     if (key == 0 || mode == 0 || tiles >= kOrderMaxTiles) return hipSuccess;
     hipError_t e;
+    // A launch on another stream than the chain's last one (TileChains: a stream beyond the
+    // kChains in use took this chain over).  That stream's handle must not be used: the caller
+    // may have destroyed it since (hipStreamQuery on a destroyed stream's handle crashed,
+    // tools/gpu/probe_dead_stream.py, profiles/r6y_dead_stream.txt), so the host waits for the
+    // whole device -- which also covers that stream's launches -- and the chain continues on s.
+    if (have_last && last_stream != s) {
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+      have_last = false;
+    }
     if (tiles > cap) {  // (re)allocate; a new chain starts
       // Stream-ordered, no device-wide wait (a hipDeviceSynchronize here had made the first draw
-      // on a new stream wait for every other stream's work): the old buffers are freed in the order
-      // of the stream of their last launch, the new ones allocated in the order of s, the stream
-      // of the launch that will use them first.
-      const hipStream_t fs = have_last ? last_stream : s;
+      // on a new stream wait for every other stream's work): the old buffers were last used on s
+      // (above), so they are freed and the new ones allocated in the order of s.
       for (int q = 0; q < 2; q++) {
-        if (order[q] && (e = hipFreeAsync(order[q], fs)) != hipSuccess) return e;
-        if (cost[q] && (e = hipFreeAsync(cost[q], fs)) != hipSuccess) return e;
+        if (order[q] && (e = hipFreeAsync(order[q], s)) != hipSuccess) return e;
+        if (cost[q] && (e = hipFreeAsync(cost[q], s)) != hipSuccess) return e;
         order[q] = nullptr;
         cost[q] = nullptr;
       }
@@ -91,11 +98,6 @@ struct TileSched {
       }
       cap = tiles;
     }
-    // A launch on another stream than the previous one: the host waits for the
-    // previous one (rare; an event recorded after every launch would instead put a
-    // marker between every two frames of the common single-stream loop).
-    if (have_last && last_stream != s && (e = hipStreamSynchronize(last_stream)) != hipSuccess)
-      return e;
     const bool same = key_prev == key;  // launch k-1 had this tile grid
     p.tile_order = (same && sorted_prev) ? order[k & 1] : nullptr;
     p.tile_cost = cost[k & 1];
@@ -148,9 +150,12 @@ struct TileSched {
 // cost or order buffer, so nothing orders them against each other -- two frames in flight
 // on two streams overlap, the second starting while the first drains.  Each chain orders
 // its launches by the march steps of its own launch two back.  A further stream takes the
-// least recently used chain, whose begin() then waits for that chain's last stream.
+// least recently used chain, whose begin() then waits for the device (a stream handle is
+// kept only to be compared, never passed to HIP: its owner may destroy it).  Sixteen chains
+// cover a render thread per stream (the reference renders with eight threads, Source.cpp:13);
+// a chain's buffers are allocated by its first launch.
 struct TileChains {
-  static constexpr int kChains = 4;
+  static constexpr int kChains = 16;
   TileSched chain[kChains];
   uint64_t clock = 0;
 

@@ -456,7 +456,9 @@ int sfrt_world_row_costs(sfrt_world* w, float* costs, int capacity, int* row0, i
   if (tile_w <= 0 || tiles_x * tiles_y > sched.cap) return SFRT_E_INVALID;
   if (capacity < L.rows) return SFRT_E_INVALID;
   sfrt::DeviceGuard g(w->device);
-  if (sched.have_last) HIP_TRY(hipStreamSynchronize(sched.last_stream));
+  // the chain's last launch may still be running on a stream the caller has since destroyed
+  // (its handle must not be used, sfrt_sched.h): a tuning call, it waits for the device
+  if (sched.have_last) HIP_TRY(hipDeviceSynchronize());
   std::vector<uint8_t> cls((size_t)(tiles_x * tiles_y));
   HIP_TRY(hipMemcpy(cls.data(), sched.cost[L.buf], cls.size(), hipMemcpyDeviceToHost));
   for (long long ty = 0; ty < tiles_y; ty++) {

@@ -226,3 +226,45 @@ def test_growth_waits_for_no_other_stream(built, floor):
         assert torch.equal(gw, again)
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+def test_destroyed_stream_is_forgotten(built, floor):
+    """A caller may destroy a stream after drawing on it (hipStreamDestroy first waits for its
+    work).  The world's tile-order chain still remembers that stream as its last one: a larger
+    frame on a seventeenth stream takes that chain over (sfrt_sched.h TileChains: sixteen chains,
+    the least recently used one taken over) and reallocates its buffers.  Neither may pass the
+    dead handle to HIP (a call on it crashed, profiles/r6y_dead_stream.txt), and the frames equal
+    the same frames rendered alone."""
+    import ctypes
+    import sfrt
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    dead = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(dead)) == 0
+    sc = scenes.default10()
+    with sfrt.World(0) as world:
+        world.load_texture(*floor)
+        world.set_scene(sc, 320, 240)
+        small = torch.empty((240, 320 * 4), dtype=torch.uint8, device="cuda:0")
+        for _ in range(3):  # the chain's first launches, on the stream about to be destroyed
+            world.render_band(small.data_ptr(), 320 * 4, 0, 240, dead.value)
+        world.check(dead.value)
+        assert hip.hipStreamDestroy(dead) == 0
+        world.set_scene(sc, 640, 480)  # more tiles than the dead stream's chain holds
+        n = 16
+        big = [torch.empty((480, 640 * 4), dtype=torch.uint8, device="cuda:0") for _ in range(n)]
+        ss = _streams(n)
+        for rep in range(2):
+            for i, s in enumerate(ss):  # the sixteenth new stream takes over the dead stream's chain
+                world.render_band(big[i].data_ptr(), 640 * 4, 0, 480, s.cuda_stream)
+        torch.cuda.synchronize()
+        for s in ss:
+            world.check(s.cuda_stream)
+        want = world.render()
+        world.set_scene(sc, 320, 240)
+        want_small = world.render()
+    assert np.array_equal(small.cpu().numpy().ravel(), want_small)
+    for i in range(n):
+        got = big[i].cpu().numpy().ravel()
+        assert np.array_equal(got, want), f"stream {i}: {_report(got, want, 640)}"
