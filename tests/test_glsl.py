@@ -20,7 +20,7 @@ import pytest
 import glsl_scenes as gs
 import oracle
 import scenes
-from conftest import ROOT, host_threads
+from conftest import ROOT, host_threads, poisoned
 
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
 
@@ -177,7 +177,7 @@ def draw_ordered(shader, u, w, h):
     per-wave wall cull), after a warm-up draw so that the tile order is in use."""
     import torch
     shader.set_uniforms(u)
-    b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+    b = poisoned((h, w * 4))
     for _ in range(3):
         shader.draw(b.data_ptr(), w, h, w * 4, 0, h, 0)
     shader.check(0)
@@ -295,7 +295,7 @@ def test_gpu_bands_tile_the_frame(shader, floor):
     u = gs.default_uniforms(w, h, 0.3, 0.1, frames=40)
     shader.set_uniforms(u)
     full = shader.draw_image(w, h)
-    buf = torch.zeros(h, w * 4 + 64, dtype=torch.uint8, device="cuda")
+    buf = poisoned((h, w * 4 + 64), 0)
     stream = torch.cuda.Stream()
     for r0 in range(0, h, 250):
         rows = min(250, h - r0)
@@ -389,7 +389,7 @@ def test_gpu_adaptive_tile_order_same_bytes(shader, floor):
     with torch.cuda.stream(stream):
         for u, w, h, r0, rows in seq:
             shader.set_uniforms(u)
-            b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            b = poisoned((h, w * 4))
             shader.draw(b[r0].data_ptr(), w, h, w * 4, r0, rows, stream.cuda_stream)
             frames.append(b)
     shader.check(stream.cuda_stream)
@@ -461,8 +461,8 @@ def test_gpu_tables_reused_across_streams(shader, floor):
     for k in range(3):
         u = gs.default_uniforms(w, h, 0.6 + 0.3 * k, 0.1, frames=5 + k)
         shader.set_uniforms(u)
-        ba = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
-        bb = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        ba = poisoned((h, w * 4))
+        bb = poisoned((h, w * 4))
         torch.cuda.synchronize()
         with torch.cuda.stream(a):
             torch.cuda._sleep(100_000_000)  # ~50 ms of queued work ahead of A's staging copy
@@ -490,7 +490,7 @@ def test_gpu_tables_restaged_after_every_uniform_setter(shader, floor):
     stream = torch.cuda.Stream()
 
     def frame():
-        b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        b = poisoned((h, w * 4))
         shader.draw(b.data_ptr(), w, h, w * 4, 0, h, stream.cuda_stream)
         shader.check(stream.cuda_stream)
         return b.cpu().numpy().ravel()
@@ -542,11 +542,11 @@ def test_gpu_ground_change_is_stream_ordered(built, floor):
         torch.cuda.synchronize()
         frames = []
         for k in range(1, len(grounds)):
-            old = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            old = poisoned((h, w * 4))
             with torch.cuda.stream(b):
                 torch.cuda._sleep(100_000_000)
             s.draw(old.data_ptr(), w, h, w * 4, 0, h, b.cuda_stream)   # reads grounds[k - 1]
-            new = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            new = poisoned((h, w * 4))
             assert not b.query(), "B drained before the calls (the test's own setup waited)"
             s.set_ground(*grounds[k])
             busy = {"set_ground": not b.query()}

@@ -25,7 +25,7 @@ import pytest
 import torch.multiprocessing as mp
 
 import scenes
-from conftest import ROOT, host_threads
+from conftest import ROOT, host_threads, poisoned
 
 pytestmark = pytest.mark.gpu
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
@@ -190,7 +190,7 @@ def _rccl_loopback_worker(_rank, lib_path, cases, out_path):
             with torch.cuda.stream(stream):
                 for p in poses:
                     m.set_camera(scene.cam_pos, *p)
-                    f = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                    f = poisoned((height, width * 4))
                     m.render(f.data_ptr(), width * 4, stream.cuda_stream)
                     frames.append(f)
             m.check()
@@ -297,7 +297,7 @@ def test_multi_render_pipelined_frames(floor_tex, n, transport):
         with torch.cuda.stream(stream):
             for p in poses:
                 m.set_camera(sc.cam_pos, *p)
-                f = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                f = poisoned((height, width * 4))
                 m.render(f.data_ptr(), width * 4, stream.cuda_stream)
                 frames.append(f)
         m.check()
@@ -640,7 +640,7 @@ def _nccl_one_rank_worker(port, key, out_path):
         w = sfrt.World(0)
         w.load_texture(*sc.load_floor())
         w.set_scene(sc.SCENES[g["scene"]]().posed(*g["pose"]), width, height)
-        frames = [torch.full((height, pitch), 0xA5, dtype=torch.uint8, device="cuda:0")
+        frames = [poisoned((height, pitch))
                   for _ in range(2)]
         band = torch.empty(height, pitch, dtype=torch.uint8, device="cuda:0")
         hashes = []

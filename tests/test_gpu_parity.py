@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import scenes
-from conftest import ROOT, host_threads
+from conftest import ROOT, host_threads, poisoned
 
 pytestmark = pytest.mark.gpu
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
@@ -122,7 +122,7 @@ def test_tile_shapes_identical(world, floor, rays):
             assert diff_report(a, b, width) == "", (sc.name, pose, "row-major")
             bufs = []
             for _ in range(3):
-                buf = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                buf = poisoned((height, width * 4))
                 torch.cuda.synchronize()
                 world.render_band(buf.data_ptr(), width * 4, 0, height, stream.cuda_stream)
                 bufs.append(buf)
@@ -351,7 +351,7 @@ def test_lcg256_ordered_frames_match_oracle(world, floor, pose):
     bufs = []
     with torch.cuda.stream(stream):
         for _ in range(4):
-            b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            b = poisoned((height, width * 4))
             world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
             bufs.append(b)
     world.check(stream.cuda_stream)
@@ -632,7 +632,7 @@ def test_adaptive_tile_order_same_bytes(world, floor):
                 ref[key] = oracle_for(scene, width, height, floor).render(host_threads())
             world.set_scene(scene, width, height)
             stream = (s1 if k % 2 == 0 else s2)
-            buf = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            buf = poisoned((height, width * 4))
             torch.cuda.synchronize()
             world.set_option(sfrt.SFRT_OPT_TILE_ORDER, 1)
             world.render_band(buf[r0].data_ptr(), width * 4, r0, rows, stream.cuda_stream)
@@ -668,7 +668,7 @@ def test_adaptive_tile_order_4k_frames(world, floor):
         for k in range(12):
             p = poses[(k // 2) % 3]
             world.set_scene(scenes.lcg64().posed(*p), width, height)
-            b = torch.full((height, width * 4), 0x5A, dtype=torch.uint8, device="cuda:0")
+            b = poisoned((height, width * 4), 0x5A)
             world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
             frames.append((p, b))
     world.check(stream.cuda_stream)
@@ -696,7 +696,7 @@ def test_adaptive_order_ragged_wide_tiles(world, floor, width, height):
         for k in range(4):
             p = poses[k // 2]
             world.set_scene(scenes.lcg64().posed(*p), width, height)
-            b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            b = poisoned((height, width * 4))
             world.render_band(b.data_ptr(), width * 4, 0, height, stream.cuda_stream)
             frames.append((p, b))
     world.check(stream.cuda_stream)
@@ -736,7 +736,7 @@ def test_division_guard_paths_match_oracle(world, floor, case):
     assert diff_report(world.render(), want, width) == ""
     for rays in (0, 4):  # 0: the kernel table's pick; 4: 32x8 tiles
         world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, rays)
-        b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        b = poisoned((height, width * 4))
         for _ in range(4):
             world.render_band(b.data_ptr(), width * 4, 0, height)
         world.check()

@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 import voxel_scenes as vs
-from conftest import ROOT, host_threads
+from conftest import ROOT, host_threads, poisoned
 
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
 
@@ -133,7 +133,7 @@ def test_voxel_adaptive_tile_order_same_bytes(vworld, assets):
         with torch.cuda.stream(stream):
             for p, r, hr, width, height, r0, rows in seq:
                 vworld.set_scene(vs.default_world(p, r, hr), width, height)
-                b = torch.full((height, width * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+                b = poisoned((height, width * 4))
                 vworld.render_band(b[r0].data_ptr(), width * 4, r0, rows, stream.cuda_stream)
                 frames.append(b)
         vworld.check(stream.cuda_stream)
@@ -164,15 +164,15 @@ def test_voxel_tables_reused_across_streams(vworld, assets):
     a, b = torch.cuda.Stream(), torch.cuda.Stream()
     base = vs.default_world((20.5, 2.2, 40.5), 1.0, 0.1)
     vworld.set_scene(base, w, h)
-    buf0 = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+    buf0 = poisoned((h, w * 4))
     vworld.render_band(buf0.data_ptr(), w * 4, 0, h, a.cuda_stream)
     vworld.check(a.cuda_stream)
     scenes_ = []
     for k in range(3):  # three scene changes: each stages a new slot on A, read at once on B
         sc = dataclasses.replace(base, cam_pos=(20.5 + 0.75 * (k + 1), 2.2, 40.5), rotation=1.0 + 0.2 * k)
         vworld.set_scene(sc, w, h)
-        ba = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
-        bb = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        ba = poisoned((h, w * 4))
+        bb = poisoned((h, w * 4))
         torch.cuda.synchronize()
         with torch.cuda.stream(a):
             torch.cuda._sleep(100_000_000)  # ~50 ms of queued work ahead of A's staging copy
@@ -202,7 +202,7 @@ def test_voxel_tables_restaged_after_every_setter(vworld, assets):
     stream = torch.cuda.Stream()
 
     def frame(w, h):
-        b = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        b = poisoned((h, w * 4))
         vworld.render_band(b.data_ptr(), w * 4, 0, h, stream.cuda_stream)
         vworld.check(stream.cuda_stream)
         return b.cpu().numpy().ravel()
@@ -289,7 +289,7 @@ def test_voxel_gpu_edge_poses_match_oracle(vworld, assets, case):
     ub = oracle.VoxelOracle.bad_texel_reads() > before
     vworld.set_scene(scene, w, h)
     stream = torch.cuda.Stream()
-    dev = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+    dev = poisoned((h, w * 4))
     vworld.render_band(dev.data_ptr(), w * 4, 0, h, stream.cuda_stream)
     if ub:
         with pytest.raises(sfrt.SfrtError) as e:
@@ -401,7 +401,7 @@ def test_voxel_gpu_random_worlds(vworld, assets):
         o = oracle.VoxelOracle(scene, w, h, assets[0], assets[1], vs.COLORS)
         want = o.render(host_threads())
         vworld.set_scene(scene, w, h)
-        dev = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        dev = poisoned((h, w * 4))
         vworld.render_band(dev.data_ptr(), w * 4, 0, h, stream.cuda_stream)
         vworld.check(stream.cuda_stream)
         g, wv = dev.cpu().numpy().reshape(-1, 4), want.reshape(-1, 4)
@@ -471,7 +471,7 @@ def test_voxel_blocks_rewrite_does_not_serialise_other_streams(built, assets):
             sphere.render_band(frame4k.data_ptr(), 3840 * 4, 0, 2160, a.cuda_stream)
         t0 = time.perf_counter()
         vworld.set_scene(second, fw, fh)
-        got = torch.full((fh, fw * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+        got = poisoned((fh, fw * 4))
         vworld.render_band(got.data_ptr(), fw * 4, 0, fh, b.cuda_stream)
         done_b = torch.cuda.Event()
         done_b.record(b)
@@ -490,12 +490,12 @@ def test_voxel_blocks_rewrite_does_not_serialise_other_streams(built, assets):
         prev = (second, fw, fh)
         for scene, sw, sh in worlds[1:] + [(vs.default_world(), 320, 180)]:
             vworld.set_scene(prev[0], prev[1], prev[2])
-            old = torch.full((prev[2], prev[1] * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            old = poisoned((prev[2], prev[1] * 4))
             with torch.cuda.stream(b):
                 torch.cuda._sleep(20_000_000)  # the old world's frame still queued behind this
             vworld.render_band(old.data_ptr(), prev[1] * 4, 0, prev[2], b.cuda_stream)
             vworld.set_scene(scene, sw, sh)
-            new = torch.full((sh, sw * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            new = poisoned((sh, sw * 4))
             vworld.render_band(new.data_ptr(), sw * 4, 0, sh, a.cuda_stream)  # rewrite on A
             torch.cuda.synchronize()
             vworld.check(a.cuda_stream)
@@ -570,7 +570,7 @@ def test_voxel_gpu_key_aliasing_matches_oracle(built, assets, name, scene):
             want = oracle.VoxelOracle(sc, w, h, assets[0], assets[1], vs.COLORS).render(host_threads())
             vw.set_scene(sc, w, h)
             stream = torch.cuda.Stream()
-            dev = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            dev = poisoned((h, w * 4))
             vw.render_band(dev.data_ptr(), w * 4, 0, h, stream.cuda_stream)
             vw.check(stream.cuda_stream)
             got = dev.cpu().numpy().ravel()
@@ -611,14 +611,14 @@ def test_voxel_texture_upload_is_stream_ordered(built, assets):
         torch.cuda.synchronize()
         frames = []
         for k in range(1, len(sets)):
-            old = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            old = poisoned((h, w * 4))
             with torch.cuda.stream(b):
                 torch.cuda._sleep(100_000_000)
             vw.render_band(old.data_ptr(), w * 4, 0, h, b.cuda_stream)    # reads sets[k - 1]
             rgba, tw, th = sets[k][0]
             vw.load_texture(0, rgba, tw, th)
             busy = not b.query()
-            new = torch.full((h, w * 4), 0xA5, dtype=torch.uint8, device="cuda:0")
+            new = poisoned((h, w * 4))
             vw.render_band(new.data_ptr(), w * 4, 0, h, a.cuda_stream)    # reads sets[k]
             frames.append((sets[k - 1], old, sets[k], new, busy))
             torch.cuda.synchronize()
