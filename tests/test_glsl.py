@@ -542,11 +542,10 @@ def test_gpu_ground_change_is_stream_ordered(built, floor):
         torch.cuda.synchronize()
         frames = []
         for k in range(1, len(grounds)):
-            old = poisoned((h, w * 4))
+            old, new = poisoned((h, w * 4)), poisoned((h, w * 4))  # filled before B is busy
             with torch.cuda.stream(b):
                 torch.cuda._sleep(100_000_000)
             s.draw(old.data_ptr(), w, h, w * 4, 0, h, b.cuda_stream)   # reads grounds[k - 1]
-            new = poisoned((h, w * 4))
             assert not b.query(), "B drained before the calls (the test's own setup waited)"
             s.set_ground(*grounds[k])
             busy = {"set_ground": not b.query()}

@@ -444,7 +444,10 @@ def test_voxel_blocks_rewrite_does_not_serialise_other_streams(built, assets):
     import scenes
     import torch
     w, h = 320, 180
-    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    # B at high priority: HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES), and two
+    # streams that share one run in order whatever the library does; a high-priority stream comes
+    # from another queue pool, so B never sits behind A's packets in hardware
+    a, b = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
     tex, tw, th = scenes.load_floor()
     sphere = sfrt.World(0)
     vworld = sfrt.VoxelWorld(0)  # its own grid: the first world allocates it, the last grows it
@@ -467,11 +470,11 @@ def test_voxel_blocks_rewrite_does_not_serialise_other_streams(built, assets):
         textured = (blocks2 >= 0) & (blocks2 != vs.EMPTY)
         blocks2[textured] = (blocks2[textured] + 1) % 4  # the same cells, other textures
         second = dataclasses.replace(first, blocks=blocks2)
+        got = poisoned((fh, fw * 4))  # filled before A is busy
         for _ in range(40):  # ~6 ms of sphere frames queued on A
             sphere.render_band(frame4k.data_ptr(), 3840 * 4, 0, 2160, a.cuda_stream)
         t0 = time.perf_counter()
         vworld.set_scene(second, fw, fh)
-        got = poisoned((fh, fw * 4))
         vworld.render_band(got.data_ptr(), fw * 4, 0, fh, b.cuda_stream)
         done_b = torch.cuda.Event()
         done_b.record(b)
@@ -611,14 +614,13 @@ def test_voxel_texture_upload_is_stream_ordered(built, assets):
         torch.cuda.synchronize()
         frames = []
         for k in range(1, len(sets)):
-            old = poisoned((h, w * 4))
+            old, new = poisoned((h, w * 4)), poisoned((h, w * 4))  # filled before B is busy
             with torch.cuda.stream(b):
                 torch.cuda._sleep(100_000_000)
             vw.render_band(old.data_ptr(), w * 4, 0, h, b.cuda_stream)    # reads sets[k - 1]
             rgba, tw, th = sets[k][0]
             vw.load_texture(0, rgba, tw, th)
             busy = not b.query()
-            new = poisoned((h, w * 4))
             vw.render_band(new.data_ptr(), w * 4, 0, h, a.cuda_stream)    # reads sets[k]
             frames.append((sets[k - 1], old, sets[k], new, busy))
             torch.cuda.synchronize()
