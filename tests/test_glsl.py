@@ -536,7 +536,9 @@ def test_gpu_ground_change_is_stream_ordered(built, floor):
     try:
         s.set_ground(*grounds[0])
         s.set_uniforms(u)
-        a, b = torch.cuda.Stream(), torch.cuda.Stream()
+        # B at high priority: the object's own stream, where the upload runs, never shares B's
+        # hardware queue (two streams that share one run in order, GPU_MAX_HW_QUEUES)
+        a, b = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
         warm = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
         s.draw(warm.data_ptr(), w, h, w * 4, 0, h, a.cuda_stream)
         torch.cuda.synchronize()

@@ -148,7 +148,9 @@ def test_growth_waits_for_no_other_stream(built, floor):
     the same frames rendered on their own afterwards."""
     import sfrt
     import torch
-    busy_stream = torch.cuda.Stream()
+    # high priority: the world's own stream (update_image) can never share its hardware queue,
+    # where it would run behind the busy work whatever the library does (GPU_MAX_HW_QUEUES)
+    busy_stream = torch.cuda.Stream(priority=-1)
     s1 = torch.cuda.Stream()
 
     def hold():

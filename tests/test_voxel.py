@@ -608,7 +608,9 @@ def test_voxel_texture_upload_is_stream_ordered(built, assets):
     try:
         vw.load_assets(sets[0], assets[1], vs.COLORS)
         vw.set_scene(scene, w, h)
-        a, b = torch.cuda.Stream(), torch.cuda.Stream()
+        # B at high priority: the object's own stream, where the upload runs, never shares B's
+        # hardware queue (two streams that share one run in order, GPU_MAX_HW_QUEUES)
+        a, b = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
         warm = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
         vw.render_band(warm.data_ptr(), w * 4, 0, h, a.cuda_stream)
         torch.cuda.synchronize()
