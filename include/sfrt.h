@@ -82,7 +82,9 @@ SFRT_API int sfrt_world_set_size(sfrt_world* w, int width, int height);         
 SFRT_API int sfrt_world_get_size(const sfrt_world* w, int* width, int* height);
 SFRT_API int sfrt_world_set_camera(sfrt_world* w, const sfrt_camera* cam);       /* SphereWorld::cam */
 SFRT_API int sfrt_world_get_camera(const sfrt_world* w, sfrt_camera* cam);
-/* textures[slot].loadFromFile(...) (SphereWorld.cpp:52): RGBA8 rows, w*h*4 bytes. Slot 0 is sampled. */
+/* textures[slot].loadFromFile(...) (SphereWorld.cpp:52): RGBA8 rows, w*h*4 bytes. Slot 0 is sampled.
+   Stream-ordered, no device-wide wait: frames queued before the call read the old texels, frames
+   queued after it (on any stream) the new ones. */
 SFRT_API int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int tex_w, int tex_h);
 /* AddSphere (SphereWorld.cpp:177-190): append, drop contained spheres, re-sort. */
 SFRT_API int sfrt_world_add_sphere(sfrt_world* w, float x, float y, float z, float radius);

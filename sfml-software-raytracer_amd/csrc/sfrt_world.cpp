@@ -130,6 +130,15 @@ struct sfrt_world {
   hipStream_t stream = nullptr;
   uint32_t* d_tex = nullptr;  // texture atlas: every loaded slot, back to back
   size_t d_tex_texels = 0;
+  // A new texture goes into a new atlas, uploaded on `stream` from pinned staging; launches
+  // queued earlier keep reading the old one (its pointer is in their arguments), launches queued
+  // later on another stream wait for the upload once (tex_written).  The old atlases are freed
+  // once the device has drained anyway (the destructor), or in one sweep per kRetiredTexBytes.
+  sfrt::SharedBuffer tex_written;
+  sfrt::PinnedStage tex_stage;
+  std::vector<void*> retired_tex;
+  size_t retired_tex_bytes = 0;
+  static constexpr size_t kRetiredTexBytes = 64u << 20;
   int* d_status = nullptr;
   sfrt::TileChains scheds;  // adaptive tile order (sfrt_sched.h), one chain per stream
   sfrt::TileSched dump_sched;  // sfrt_world_trace_points' own chain (never the frames')
@@ -182,6 +191,9 @@ struct sfrt_world {
     scheds.release();
     dump_sched.release();
     (void)hipFree(d_tex);
+    for (void* p : retired_tex) (void)hipFree(p);
+    tex_written.release();
+    tex_stage.release();
     (void)hipFree(d_status);
     (void)hipDeviceSynchronize();
     for (int k = 0; k < kRing; k++) {
@@ -558,18 +570,34 @@ int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int te
   }
   if (total > 0xffffffffull) return SFRT_E_INVALID;
   sfrt::DeviceGuard g(w->device);
-  HIP_TRY(hipDeviceSynchronize());
-  if (w->d_tex_texels < total) {
-    (void)hipFree(w->d_tex);
-    w->d_tex = nullptr;
-    w->d_tex_texels = 0;
-    HIP_TRY(hipMalloc(&w->d_tex, total * 4));
-    w->d_tex_texels = total;
-  }
+  // Stream-ordered (no device-wide wait): a new atlas (hipMalloc waits for no stream,
+  // profiles/r6u_hip_alloc_calls.txt), uploaded on the world's stream from pinned staging.
+  std::vector<uint8_t> atlas(total * 4);
   for (int k = 0; k < SFRT_TEXTURE_SLOTS; k++)
     if (!w->tex_host[k].empty())
-      HIP_TRY(hipMemcpy(w->d_tex + w->tex_off[k], w->tex_host[k].data(), w->tex_host[k].size(),
-                        hipMemcpyHostToDevice));
+      std::memcpy(atlas.data() + (size_t)w->tex_off[k] * 4, w->tex_host[k].data(), w->tex_host[k].size());
+  void* staged = nullptr;
+  HIP_TRY(w->tex_stage.fill(atlas.data(), atlas.size(), &staged));
+  uint32_t* fresh = nullptr;
+  HIP_TRY(hipMalloc(&fresh, total * 4));
+  if (hipMemcpyAsync(fresh, staged, total * 4, hipMemcpyHostToDevice, w->stream) != hipSuccess ||
+      w->tex_stage.copied(w->stream) != hipSuccess || w->tex_written.after_write(w->stream) != hipSuccess) {
+    (void)hipStreamSynchronize(w->stream);
+    (void)hipFree(fresh);
+    return SFRT_E_HIP;
+  }
+  if (w->d_tex) {
+    w->retired_tex.push_back(w->d_tex);
+    w->retired_tex_bytes += w->d_tex_texels * 4;
+  }
+  w->d_tex = fresh;
+  w->d_tex_texels = total;
+  if (w->retired_tex_bytes > sfrt_world::kRetiredTexBytes) {  // a texture reloaded every frame
+    HIP_TRY(hipDeviceSynchronize());
+    for (void* p : w->retired_tex) (void)hipFree(p);
+    w->retired_tex.clear();
+    w->retired_tex_bytes = 0;
+  }
   return SFRT_OK;
 }
 
@@ -766,6 +794,8 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   f.out_pitch = pitch_bytes / 4;
   rc = w->stage_spheres(f, recs, s, false);
   if (rc) return rc;
+  // after the last texture upload (queued on w->stream, where the other launches run)
+  HIP_TRY(w->tex_written.before_read(s));
   if ((rc = w->sched_begin(f, s))) return rc;
   if ((rc = w->sched_end(f, s, sfrt::launch_trace(f, recs.data(), s, nullptr, w->ring_event()) == 0)))
     return rc;

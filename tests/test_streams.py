@@ -13,6 +13,7 @@ import pytest
 import glsl_scenes as gs
 import scenes
 import voxel_scenes as vs
+from conftest import poisoned
 
 
 def _report(got, want, w):
@@ -270,3 +271,51 @@ def test_destroyed_stream_is_forgotten(built, floor):
     for i in range(n):
         got = big[i].cpu().numpy().ravel()
         assert np.array_equal(got, want), f"stream {i}: {_report(got, want, 640)}"
+
+
+@pytest.mark.gpu
+def test_sphere_texture_load_is_stream_ordered(built, floor):
+    """sfrt_world_load_texture without a device-wide wait: the new texels go into a new atlas,
+    uploaded on the world's own stream, so a frame queued earlier on another stream (here behind
+    ~50 ms of work on B) still reads the texels it was queued with and the call does not wait for
+    it; a frame queued after the call, on another stream, reads the new ones.  A larger texture
+    and a return to the first one included.  Each frame equals the same frame rendered on its own
+    by a second world holding only that texture."""
+    import sfrt
+    import torch
+    w, h = 320, 240
+    rng = np.random.default_rng(5)
+    texs = [floor, (rng.integers(0, 256, 128 * 128 * 4, dtype=np.uint8), 128, 128),
+            (rng.integers(0, 256, 256 * 256 * 4, dtype=np.uint8), 256, 256), floor]
+    sc = scenes.lcg64()
+    # B at high priority: the world's stream, where the upload runs, never shares its hardware
+    # queue (two streams that share one run in order, GPU_MAX_HW_QUEUES)
+    a, b = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
+    frames = []
+    with sfrt.World(0) as world:
+        world.load_texture(*texs[0])
+        world.set_scene(sc, w, h)
+        warm = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
+        world.render_band(warm.data_ptr(), w * 4, 0, h, a.cuda_stream)
+        torch.cuda.synchronize()
+        for k in range(1, len(texs)):
+            old, new = poisoned((h, w * 4)), poisoned((h, w * 4))
+            with torch.cuda.stream(b):
+                torch.cuda._sleep(100_000_000)
+            world.render_band(old.data_ptr(), w * 4, 0, h, b.cuda_stream)  # reads texs[k - 1]
+            world.load_texture(*texs[k])
+            busy = not b.query()
+            world.render_band(new.data_ptr(), w * 4, 0, h, a.cuda_stream)  # reads texs[k]
+            frames.append((texs[k - 1], old, texs[k], new, busy))
+            torch.cuda.synchronize()
+        world.check(a.cuda_stream)
+        world.check(b.cuda_stream)
+    for t_old, old, t_new, new, busy in frames:
+        assert busy, "load_texture waited for the queued frame on B"
+        for t, buf in ((t_old, old), (t_new, new)):
+            with sfrt.World(0) as ref:
+                ref.load_texture(*t)
+                ref.set_scene(sc, w, h)
+                want = ref.render()
+            got = buf.cpu().numpy().ravel()
+            assert np.array_equal(got, want), _report(got, want, w)
