@@ -199,6 +199,12 @@ struct PinnedStage {
 
   // The staging buffer holding a copy of src[0, bytes).
   hipError_t fill(const void* src, size_t bytes, void** out) {
+    const hipError_t e = take(bytes, out);
+    if (e == hipSuccess) std::memcpy(*out, src, bytes);
+    return e;
+  }
+  // The staging buffer, room for `bytes`, for the caller to write (its last copy has run).
+  hipError_t take(size_t bytes, void** out) {
     hipError_t e;
     if (pending) {
       if ((e = hipEventSynchronize(ev)) != hipSuccess) return e;
@@ -213,7 +219,6 @@ struct PinnedStage {
       cap = c;
     }
     if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
-    std::memcpy(h, src, bytes);
     *out = h;
     return hipSuccess;
   }

@@ -572,12 +572,12 @@ int sfrt_world_load_texture(sfrt_world* w, int slot, const uint8_t* rgba, int te
   sfrt::DeviceGuard g(w->device);
   // Stream-ordered (no device-wide wait): a new atlas (hipMalloc waits for no stream,
   // profiles/r6u_hip_alloc_calls.txt), uploaded on the world's stream from pinned staging.
-  std::vector<uint8_t> atlas(total * 4);
+  void* staged = nullptr;
+  HIP_TRY(w->tex_stage.take(total * 4, &staged));
   for (int k = 0; k < SFRT_TEXTURE_SLOTS; k++)
     if (!w->tex_host[k].empty())
-      std::memcpy(atlas.data() + (size_t)w->tex_off[k] * 4, w->tex_host[k].data(), w->tex_host[k].size());
-  void* staged = nullptr;
-  HIP_TRY(w->tex_stage.fill(atlas.data(), atlas.size(), &staged));
+      std::memcpy((uint8_t*)staged + (size_t)w->tex_off[k] * 4, w->tex_host[k].data(),
+                  w->tex_host[k].size());
   uint32_t* fresh = nullptr;
   HIP_TRY(hipMalloc(&fresh, total * 4));
   if (hipMemcpyAsync(fresh, staged, total * 4, hipMemcpyHostToDevice, w->stream) != hipSuccess ||
