@@ -169,6 +169,10 @@ struct Rank {
   hipEvent_t rendered[2] = {}, copied[2] = {};
   bool copy_pending[2] = {};
   ncclComm_t comm = nullptr;
+  // Replaced buffers, freed with the object: hipFree waits for the whole device (sfrt_host.h),
+  // and the capacities grow geometrically, so these stay below the live ones.
+  std::vector<void*> retired;        // on its device
+  std::vector<void*> retired_stage;  // on devices[0]
 };
 
 }  // namespace
@@ -187,6 +191,7 @@ struct sfrt_multi {
   hipStream_t out_s = nullptr;  // devices[0]: update_image's frame stream
   uint8_t* d_frame = nullptr;   // devices[0]: update_image's frame
   size_t d_frame_bytes = 0;
+  std::vector<void*> retired_frames;  // replaced d_frame buffers (see Rank::retired)
   std::mutex mu;
 
   ~sfrt_multi() {
@@ -205,14 +210,17 @@ struct sfrt_multi {
         if (r.rendered[q]) (void)hipEventDestroy(r.rendered[q]);
         if (r.copied[q]) (void)hipEventDestroy(r.copied[q]);
       }
+      for (void* p : r.retired) (void)hipFree(p);
       if (r.render_s) (void)hipStreamDestroy(r.render_s);
       if (r.copy_s) (void)hipStreamDestroy(r.copy_s);
       sfrt_world_destroy(r.world);
     }
     if (!ranks.empty()) {
       sfrt::DeviceGuard g(ranks[0].device);
-      for (Rank& r : ranks)
+      for (Rank& r : ranks) {
         for (int q = 0; q < 2; q++) (void)hipFree(r.stage[q]);
+        for (void* p : r.retired_stage) (void)hipFree(p);
+      }
       for (int q = 0; q < 2; q++)
         if (unpacked[q]) (void)hipEventDestroy(unpacked[q]);
       if (out_s) {
@@ -220,6 +228,7 @@ struct sfrt_multi {
         (void)hipStreamDestroy(out_s);
       }
       (void)hipFree(d_frame);
+      for (void* p : retired_frames) (void)hipFree(p);
       if (start) (void)hipEventDestroy(start);
     }
   }
@@ -251,7 +260,8 @@ struct sfrt_multi {
   }
 
   // Packed transfer buffers for bands of rows[r] x width pixels: rank r's packed[2] on
-  // its device, stage[2] on devices[0].  Growing them first drains every stream.
+  // its device, stage[2] on devices[0].  Growing them first drains this object's streams; the
+  // old buffers are retired (Rank::retired), not freed.
   int packed_buffers(const std::vector<int>& rows, int width) {
     for (size_t r = 1; r < ranks.size(); r++) {
       Rank& R = ranks[r];
@@ -263,24 +273,25 @@ struct sfrt_multi {
         HIP_TRY(hipStreamSynchronize(Q.render_s));
         HIP_TRY(hipStreamSynchronize(Q.copy_s));
       }
+      const size_t cap = sfrt::grown_capacity(R.packed_bytes, (size_t)b);
       {
         sfrt::DeviceGuard g(R.device);
         for (int q = 0; q < 2; q++) {
-          (void)hipFree(R.packed[q]);
+          if (R.packed[q]) R.retired.push_back(R.packed[q]);
           R.packed[q] = nullptr;
         }
         R.packed_bytes = 0;
-        for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.packed[q], (size_t)b));
+        for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.packed[q], cap));
       }
       {
         sfrt::DeviceGuard g(ranks[0].device);
         for (int q = 0; q < 2; q++) {
-          (void)hipFree(R.stage[q]);
+          if (R.stage[q]) R.retired_stage.push_back(R.stage[q]);
           R.stage[q] = nullptr;
         }
-        for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.stage[q], (size_t)b));
+        for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.stage[q], cap));
       }
-      R.packed_bytes = (size_t)b;
+      R.packed_bytes = cap;
     }
     return SFRT_OK;
   }
@@ -328,14 +339,15 @@ struct sfrt_multi {
         if (R.band_bytes < bytes) {
           HIP_TRY(hipStreamSynchronize(R.render_s));
           HIP_TRY(hipStreamSynchronize(R.copy_s));
+          const size_t cap = sfrt::grown_capacity(R.band_bytes, bytes);
           for (int q = 0; q < 2; q++) {
-            (void)hipFree(R.band[q]);
+            if (R.band[q]) R.retired.push_back(R.band[q]);  // not freed: Rank::retired
             R.band[q] = nullptr;
             R.copy_pending[q] = false;
           }
           R.band_bytes = 0;
-          for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.band[q], bytes));
-          R.band_bytes = bytes;
+          for (int q = 0; q < 2; q++) HIP_TRY(hipMalloc(&R.band[q], cap));
+          R.band_bytes = cap;
         }
         // the transfer that last read this buffer must be done before it is overwritten
         if (R.copy_pending[slot]) HIP_TRY(hipStreamWaitEvent(R.render_s, R.copied[slot], 0));
@@ -707,11 +719,12 @@ int sfrt_multi_update_image(sfrt_multi* m, uint8_t* pixels) {
   sfrt::DeviceGuard g(m->ranks[0].device);
   if (m->d_frame_bytes < bytes) {
     HIP_TRY(hipStreamSynchronize(m->out_s));
-    (void)hipFree(m->d_frame);
+    if (m->d_frame) m->retired_frames.push_back(m->d_frame);  // not freed: Rank::retired
     m->d_frame = nullptr;
     m->d_frame_bytes = 0;
-    HIP_TRY(hipMalloc(&m->d_frame, bytes));
-    m->d_frame_bytes = bytes;
+    const size_t cap = sfrt::grown_capacity(0, bytes);
+    HIP_TRY(hipMalloc(&m->d_frame, cap));
+    m->d_frame_bytes = cap;
   }
   if ((rc = m->render(m->d_frame, (int64_t)width * 4, m->out_s))) return rc;
   HIP_TRY(hipMemcpyAsync(pixels, m->d_frame, bytes, hipMemcpyDeviceToHost, m->out_s));
