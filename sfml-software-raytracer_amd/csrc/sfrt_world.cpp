@@ -422,11 +422,16 @@ struct sfrt_world {
   };
   ChainCam chain_cam[sfrt::TileChains::kChains];  // per chain
 
+  // On s itself: hipMemcpy / hipMemset run on the null stream, which also waits for every blocking
+  // stream of the process (a caller's hipStreamCreate streams), not just s.
   int read_status(hipStream_t s) {
-    HIP_TRY(hipStreamSynchronize(s));
     int st = 0;
-    HIP_TRY(hipMemcpy(&st, d_status, sizeof(int), hipMemcpyDeviceToHost));
-    if (st) HIP_TRY(hipMemset(d_status, 0, sizeof(int)));
+    HIP_TRY(hipMemcpyAsync(&st, d_status, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (st) {
+      HIP_TRY(hipMemsetAsync(d_status, 0, sizeof(int), s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
     if (st & 1) return SFRT_E_MARCH_LIMIT;
     if (st & 2) return SFRT_E_TEXEL;
     return SFRT_OK;

@@ -319,3 +319,50 @@ def test_sphere_texture_load_is_stream_ordered(built, floor):
                 want = ref.render()
             got = buf.cpu().numpy().ravel()
             assert np.array_equal(got, want), _report(got, want, w)
+
+
+@pytest.mark.gpu
+def test_check_waits_for_no_other_stream(built, floor):
+    """check() reads a frame's status on the caller's stream.  A hipMemcpy there ran on the null
+    stream, which also waits for every *blocking* stream of the process (hipStreamCreate's
+    default, as a C++ caller of the ABI would create them) -- here one holding ~50 ms of work,
+    at high priority so that no other stream shares its hardware queue."""
+    import ctypes
+    import sfrt
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    blk = ctypes.c_void_p()
+    assert hip.hipStreamCreateWithPriority(ctypes.byref(blk), 0, -1) == 0  # flags 0: blocking
+    ext = torch.cuda.ExternalStream(blk.value)
+    s1 = torch.cuda.Stream()
+    w, h = 320, 240
+    buf = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
+    busy = {}
+    tex, dyn = vs.load_textures()
+    world, vw, g = sfrt.World(0), sfrt.VoxelWorld(0), sfrt.GlslShader(0)
+    try:
+        world.load_texture(*floor)
+        world.set_scene(scenes.default10(), w, h)
+        vw.load_assets(tex, dyn, vs.COLORS)
+        vw.set_scene(vs.default_world((20.5, 2.2, 40.5), 1.0, 0.1), w, h)
+        g.set_ground(*floor)
+        g.set_uniforms(gs.default_uniforms(w, h, 0.4, 0.1))
+        draws = {"sphere": lambda: world.render_band(buf.data_ptr(), w * 4, 0, h, s1.cuda_stream),
+                 "voxel": lambda: vw.render_band(buf.data_ptr(), w * 4, 0, h, s1.cuda_stream),
+                 "glsl": lambda: g.draw(buf.data_ptr(), w, h, w * 4, 0, h, s1.cuda_stream)}
+        checks = {"sphere": world.check, "voxel": vw.check, "glsl": g.check}
+        for name, draw in draws.items():
+            draw()
+            s1.synchronize()
+            with torch.cuda.stream(ext):
+                torch.cuda._sleep(100_000_000)
+            checks[name](s1.cuda_stream)
+            busy[name] = not ext.query()
+            ext.synchronize()
+    finally:
+        torch.cuda.synchronize()
+        world.close()
+        vw.close()
+        g.close()
+        assert hip.hipStreamDestroy(blk) == 0
+    assert all(busy.values()), f"check() waited for an unrelated blocking stream: {busy}"
