@@ -140,6 +140,8 @@ SFRT_API int sfrt_world_row_costs(sfrt_world* w, float* costs, int capacity, int
 SFRT_API int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket);
 SFRT_API int sfrt_world_wait_frame(sfrt_world* w, int64_t ticket);
 SFRT_API int sfrt_host_alloc(void** ptr, int64_t bytes);
+/* hipHostFree underneath: it returns only once the whole device is idle (profiles/r6u_hip_alloc_calls.txt),
+   so free pinned frames at shutdown or between bursts, not between frames. */
 SFRT_API int sfrt_host_free(void* ptr);
 
 /* Float intermediates for `count` pixels (ij = i0, j0, i1, j1, ...), synchronous: the
