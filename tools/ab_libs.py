@@ -79,10 +79,9 @@ def renderer(sfrt, scenes, sname, pose, width, height, rays):
 
 def child(cases, reps, rays):
     sys.path.insert(0, os.path.join(ROOT, "sfml-software-raytracer_amd"))
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import torch
-    import oracle
+    import hashlib
     import scenes
     import sfrt
     stream = torch.cuda.Stream()
@@ -137,7 +136,7 @@ def child(cases, reps, rays):
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / reps
         out[name] = {"us": round((t[len(t) // 2] - gap) * 1e3, 2), "wall_us": round(wall * 1e6, 2),
-                     "fnv": oracle.fnv1a64(buf.cpu().numpy())}
+                     "fnv": hashlib.sha256(buf.cpu().numpy().tobytes()).hexdigest()[:16]}
     print("RESULT " + json.dumps(out), flush=True)
 
 
