@@ -383,8 +383,10 @@ __device__ __forceinline__ void fragment(const GlslFrame& f, const_ptr<GlslWall>
         const GlslPair P = ld(as_const(f.pairs), li * nshadow + k);
         const float cosang = (-tnx * P.ux + -tny * P.uy) + -tnz * P.uz;
         // Ball outside the light cone seen from pos: acos(cosang) >= sanglet
-        // (with margin) makes the clamp's argument >= 1, factor 1 exactly.
-        if (!__builtin_amdgcn_ballot_w64(!(near && cosang <= P.cos_lit))) continue;
+        // (with margin) makes the clamp's argument >= 1, factor 1 exactly.  Not below -1:
+        // a rounded cosang of -1.0000001 (a ball straight behind pos from the light) makes
+        // acos NaN and the shader's clamp passes NaN on (its brightness, then the pixel, 0).
+        if (!__builtin_amdgcn_ballot_w64(!(near && cosang <= P.cos_lit && cosang >= -1.0f))) continue;
         float sangle = sfrt_math::acosf(cosang);
         const float psd = 1.5f / (0.8f + 0.2f * len3(px - P.bx, py - P.by, pz - P.bz));
         sangle = sangle * psd - (psd - 1.0f) * P.sanglet;

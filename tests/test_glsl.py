@@ -215,6 +215,51 @@ def test_gpu_wall_cull_random_scenes(shader, floor):
         assert np.array_equal(got, want), (seed, nw, first_diff(got, want, w))
 
 
+def _sweep_uniforms(seed):
+    """The uniforms scene `seed` of tests/test_parity_sweep.py's GLSL sweep draws (its random
+    sequence replayed from the first scene)."""
+    rng = np.random.default_rng(20000)
+    for s in range(20000, seed + 1):
+        nw, nl, nb = int(rng.integers(3, 61)), int(rng.integers(0, 4)), int(rng.integers(0, 12))
+        w, h = [(160, 90), (96, 64), (133, 47)][s % 3]
+        fov = (np.float32(rng.uniform(1.5, 2.6)), np.float32(rng.uniform(1.0, 2.0))) if s % 4 == 0 else None
+    u = gs.random_uniforms(seed, nw, nl, nb, w, h)
+    if fov is not None:
+        u["fov"] = fov
+    return u, w, h
+
+
+# (seed, pixel): a shadow ball whose cosine to the light rounds to -1.0000001 there
+SHADOW_NAN_CASES = [(20904, (143, 25)), (23983, (38, 23))]
+
+
+@pytest.mark.parametrize("case", SHADOW_NAN_CASES, ids=[str(c[0]) for c in SHADOW_NAN_CASES])
+def test_oracle_shadow_cosine_below_minus_one_is_nan(floor, case):
+    """The restatement's semantics at the edge the parity sweep found (profiles/r6ps_*): a
+    shadow ball straight behind the point from the light gives dot(-tolightnorm, u) =
+    -1.0000001 in binary32, acos (glibc acosf) is NaN, the GLSL clamp formula passes NaN on,
+    and the pixel's colour converts to 0."""
+    seed, (x, y) = case
+    u, w, h = _sweep_uniforms(seed)
+    d = oracle.GlslOracle(u, *floor).pixel(w, h, x, y)
+    assert np.isnan(d["brightness"]) and d["color"][3] == 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", SHADOW_NAN_CASES, ids=[str(c[0]) for c in SHADOW_NAN_CASES])
+def test_gpu_shadow_cosine_below_minus_one(shader, floor, case):
+    """The kernel's exact shadow skip (cosang <= cos_lit: the clamp's argument >= 1) must not
+    take a cosine below -1, whose acos is NaN: both kernels equal the oracle on the two scenes
+    of the 10,000-scene sweep that had one such pixel each."""
+    seed, _ = case
+    u, w, h = _sweep_uniforms(seed)
+    want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
+    got = draw_ordered(shader, u, w, h)
+    assert np.array_equal(got, want), first_diff(got, want, w)
+    got = draw(shader, u, w, h)
+    assert np.array_equal(got, want), first_diff(got, want, w)
+
+
 @pytest.mark.gpu
 def test_gpu_synthetic_ground_mips(shader, floor):
     """Non-square ground (64x32: 2x1 box levels) over the default uniforms."""
