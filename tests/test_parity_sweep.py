@@ -5,9 +5,12 @@ tests use, every frame against the CPU restatement byte for byte --
 * sphere world: tests/test_gpu_parity.py `_fuzz_scene` (sphere counts on both sides of every
   kernel switch, cameras at centres / inside / near surfaces / outside, any pose and field of
   view, ragged frames), the default kernel table and, for every fourth scene, 32x8 tiles forced;
+  a third of the scenes through render_band with the adaptive tile order, the rest row-major;
 * GLSL mode: `glsl_scenes.random_uniforms` (3-60 walls, 0-3 lights, 0-11 balls, a quarter with a
-  wide field of view) through the ordered kernel (adaptive tile order, wall cull);
-* voxel World: `voxel_scenes.random_world` (grids, billboards, lights and shadows, view distances).
+  wide field of view) through the ordered kernel (adaptive tile order, wall cull), and every
+  second scene through the row-major kernel (draw_image) as well;
+* voxel World: `voxel_scenes.random_world` (grids, billboards, lights and shadows, view distances),
+  every second scene with the adaptive tile order.
 
 The summary (scenes, pixels and mismatches per renderer) goes to $SFRT_PARITY_SWEEP_OUT
 (profiles/r6ps_parity_sweep.json is one such run).
@@ -53,7 +56,14 @@ def test_sphere_sweep(built, floor):
             sc, w, h = _fuzz_scene(seed)
             world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 4 if seed % 4 == 0 else 0)
             world.set_scene(sc, w, h)
-            got = world.render()
+            if seed % 3 == 1:  # render_band: the adaptive tile order in use from the third frame
+                b = poisoned((h, w * 4))
+                for _ in range(3):
+                    world.render_band(b.data_ptr(), w * 4, 0, h, 0)
+                world.check(0)
+                got = b.cpu().numpy().ravel()
+            else:  # update_image: row-major
+                got = world.render()
             want = oracle.Oracle.from_scene(sc, w, h, *floor).render(host_threads())
             msg = diff_report(got, want, w)
             if msg:
@@ -88,6 +98,11 @@ def test_glsl_sweep(built, floor):
             if not np.array_equal(got, want):
                 n = int(np.count_nonzero(np.any(got.reshape(-1, 4) != want.reshape(-1, 4), axis=1)))
                 bad.append({"seed": seed, "walls": nw, "pixels_differ": n})
+            elif seed % 2 == 1:  # and the row-major kernel without the wall cull (draw_image)
+                got = s.draw_image(w, h)
+                if not np.array_equal(got, want):
+                    n = int(np.count_nonzero(np.any(got.reshape(-1, 4) != want.reshape(-1, 4), axis=1)))
+                    bad.append({"seed": seed, "walls": nw, "pixels_differ": n, "kernel": "row-major"})
             pixels += w * h
             _progress("glsl", seed - 20000 + 1, bad)
     finally:
@@ -106,9 +121,11 @@ def test_voxel_sweep(built):
         v.load_assets(tex, dyn, vs.COLORS)
         for seed in range(20000, 20000 + N):
             scene, w, h = vs.random_world(seed)
+            v.set_option(sfrt.SFRT_OPT_TILE_ORDER, seed % 2)  # off by default; on: LPT order
             v.set_scene(scene, w, h)
             b = poisoned((h, w * 4))
-            v.render_band(b.data_ptr(), w * 4, 0, h, 0)
+            for _ in range(1 + 2 * (seed % 2)):  # the order in use from the third frame
+                v.render_band(b.data_ptr(), w * 4, 0, h, 0)
             v.check(0)
             got = b.cpu().numpy().ravel()
             want = oracle.VoxelOracle(scene, w, h, tex, dyn, vs.COLORS).render(host_threads())
