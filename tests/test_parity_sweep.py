@@ -43,6 +43,10 @@ def _progress(name, i, bad):
 def _record(name, scenes, pixels, bad, skipped=0):
     RESULTS[name] = {"scenes": scenes, "pixels": pixels, "mismatched_scenes": bad,
                      "skipped_march_cap_both_sides": skipped, "mode": MODE}
+    _record_flush()
+
+
+def _record_flush():
     out = os.environ.get("SFRT_PARITY_SWEEP_OUT")
     if out:
         with open(out, "w") as f:
@@ -241,7 +245,7 @@ def test_voxel_sweep(built):
     import oracle
     import sfrt
     tex, dyn = vs.load_textures()
-    bad, pixels = [], 0
+    bad, pixels, ub = [], 0, 0
     v = sfrt.VoxelWorld(0)
     try:
         v.load_assets(tex, dyn, vs.COLORS)
@@ -252,13 +256,22 @@ def test_voxel_sweep(built):
             b = poisoned((h, w * 4))
             for _ in range(1 + 2 * (seed % 2)):  # the order in use from the third frame
                 v.render_band(b.data_ptr(), w * 4, 0, h, 0)
+            flagged = False
             try:
                 v.check(0)
-            except sfrt.SfrtError as e:
-                bad.append({"seed": seed, "error": str(e)})
-                continue
+            except sfrt.SfrtError as e:  # SFRT_E_TEXEL: the reference reads outside a texture
+                if e.code != -7:  # SFRT_E_TEXEL
+                    bad.append({"seed": seed, "error": str(e)})
+                    continue
+                flagged = True
             got = b.cpu().numpy().ravel()
+            before = oracle.VoxelOracle.bad_texel_reads()
             want = oracle.VoxelOracle(scene, w, h, tex, dyn, vs.COLORS).render(host_threads())
+            oob = oracle.VoxelOracle.bad_texel_reads() > before
+            if flagged != oob:  # both read the same stand-in texel, and both must say so
+                bad.append({"seed": seed, "texel_outside": {"gpu": flagged, "oracle": oob}})
+            elif flagged:
+                ub += 1
             if not np.array_equal(got, want):
                 n = int(np.count_nonzero(np.any(got.reshape(-1, 4) != want.reshape(-1, 4), axis=1)))
                 bad.append({"seed": seed, "pixels_differ": n})
@@ -267,4 +280,6 @@ def test_voxel_sweep(built):
     finally:
         v.close()
     _record("voxel", N, pixels, bad)
+    RESULTS["voxel"]["texel_outside_both_sides"] = ub  # reference UB, stand-in texel on both
+    _record_flush()
     assert not bad, bad[:3]
