@@ -30,13 +30,19 @@ N = int(os.environ.get("SFRT_PARITY_SWEEP", "0"))
 # "adversarial": the same generators pushed to their degenerate corners (below)
 MODE = os.environ.get("SFRT_PARITY_SWEEP_MODE", "random")
 SEED0 = 20000 if MODE == "random" else 50000
+# "WxH": every scene at that frame size instead of the generators' small ragged ones (a 4K
+# sweep reaches the kernels' large-frame choices: 32x8 tiles by the tile count, ordered launches)
+SIZE = tuple(int(v) for v in os.environ["SFRT_PARITY_SWEEP_SIZE"].split("x")) \
+    if os.environ.get("SFRT_PARITY_SWEEP_SIZE") else None
+if SIZE:
+    SEED0 += 100000
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(N <= 0, reason="on demand: SFRT_PARITY_SWEEP=<scenes per renderer>")]
 RESULTS = {}
 
 
 def _progress(name, i, bad):
-    if i % 25 == 0:  # a line now and then: a long sweep must not look hung
+    if i % 25 == 0 or SIZE:  # a line now and then: a long sweep must not look hung
         print(f"{name}: {i} of {N} scenes, {len(bad)} mismatched", flush=True)
 
 
@@ -165,6 +171,7 @@ def test_sphere_sweep(built, floor):
         world.load_texture(*floor)
         for seed in range(SEED0, SEED0 + N):
             sc, w, h = _fuzz_scene(seed) if MODE == "random" else _sphere_adversarial(seed)
+            w, h = SIZE or (w, h)
             world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 4 if seed % 4 == 0 else 0)
             world.set_scene(sc, w, h)
             try:
@@ -199,7 +206,7 @@ def test_glsl_sweep(built, floor):
         s.set_ground(*floor)
         for seed in range(SEED0, SEED0 + N):
             nw, nl, nb = int(rng.integers(3, 61)), int(rng.integers(0, 4)), int(rng.integers(0, 12))
-            w, h = [(160, 90), (96, 64), (133, 47)][seed % 3]
+            w, h = SIZE or [(160, 90), (96, 64), (133, 47)][seed % 3]
             if MODE == "random":
                 u = gs.random_uniforms(seed, nw, nl, nb, w, h)
             else:
@@ -251,6 +258,7 @@ def test_voxel_sweep(built):
         v.load_assets(tex, dyn, vs.COLORS)
         for seed in range(SEED0, SEED0 + N):
             scene, w, h = vs.random_world(seed) if MODE == "random" else _voxel_adversarial(seed)
+            w, h = SIZE or (w, h)
             v.set_option(sfrt.SFRT_OPT_TILE_ORDER, seed % 2)  # off by default; on: LPT order
             v.set_scene(scene, w, h)
             b = poisoned((h, w * 4))
