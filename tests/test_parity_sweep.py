@@ -12,6 +12,7 @@ tests use, every frame against the CPU restatement byte for byte --
 * voxel World: `voxel_scenes.random_world` (grids, billboards, lights and shadows, view distances),
   every second scene with the adaptive tile order.
 
+Every fifth scene is drawn as 2-4 random row bands (global row indices, as the multi-GPU bands).
 The summary (scenes, pixels and mismatches per renderer) goes to $SFRT_PARITY_SWEEP_OUT
 (profiles/r6ps_parity_sweep.json is one such run).
     SFRT_PARITY_SWEEP=1000 python -m pytest tests/test_parity_sweep.py -m gpu
@@ -57,6 +58,17 @@ def _record_flush():
     if out:
         with open(out, "w") as f:
             json.dump({"per_renderer": RESULTS, "scenes_per_renderer": N}, f, indent=1)
+
+
+def _bands(seed, h):
+    """Row bands [(row0, rows), ...] of an h-row frame: 2-4 random cuts for every fifth scene
+    (seed % 5 == 2; global row indices, as the multi-GPU bands use them), else the whole frame."""
+    if seed % 5 != 2 or h < 4:
+        return [(0, h)]
+    rng = np.random.default_rng(seed + 3)
+    cuts = sorted(set(int(c) for c in rng.integers(1, h, int(rng.integers(1, 4)))))
+    edges = [0] + cuts + [h]
+    return [(a, b - a) for a, b in zip(edges, edges[1:])]
 
 
 F = np.float32
@@ -175,10 +187,11 @@ def test_sphere_sweep(built, floor):
             world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 4 if seed % 4 == 0 else 0)
             world.set_scene(sc, w, h)
             try:
-                if seed % 3 == 1:  # render_band: the adaptive tile order in use from the third frame
-                    b = poisoned((h, w * 4))
+                if seed % 3 == 1 or seed % 5 == 2:  # render_band (the adaptive tile order in use
+                    b = poisoned((h, w * 4))        # from the third frame), in row bands at times
                     for _ in range(3):
-                        world.render_band(b.data_ptr(), w * 4, 0, h, 0)
+                        for r0, n in _bands(seed, h):
+                            world.render_band(b[r0].data_ptr(), w * 4, r0, n, 0)
                     world.check(0)
                     got = b.cpu().numpy().ravel()
                 else:  # update_image: row-major
@@ -215,8 +228,9 @@ def test_glsl_sweep(built, floor):
                 u["fov"] = (np.float32(rng.uniform(1.5, 2.6)), np.float32(rng.uniform(1.0, 2.0)))
             s.set_uniforms(u)
             b = poisoned((h, w * 4))
-            for _ in range(3):  # the adaptive order in use from the third draw
-                s.draw(b.data_ptr(), w, h, w * 4, 0, h, 0)
+            for _ in range(3):  # the adaptive order in use from the third draw; row bands at times
+                for r0, n in _bands(seed, h):
+                    s.draw(b[r0].data_ptr(), w, h, w * 4, r0, n, 0)
             try:
                 want = oracle.GlslOracle(u, *floor).render(w, h, host_threads())
             except RuntimeError:  # the restatement's march cap: no defined frame to compare
@@ -263,7 +277,8 @@ def test_voxel_sweep(built):
             v.set_scene(scene, w, h)
             b = poisoned((h, w * 4))
             for _ in range(1 + 2 * (seed % 2)):  # the order in use from the third frame
-                v.render_band(b.data_ptr(), w * 4, 0, h, 0)
+                for r0, n in _bands(seed, h):
+                    v.render_band(b[r0].data_ptr(), w * 4, r0, n, 0)
             flagged = False
             try:
                 v.check(0)
