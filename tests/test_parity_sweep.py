@@ -6,6 +6,7 @@ tests use, every frame against the CPU restatement byte for byte --
   kernel switch, cameras at centres / inside / near surfaces / outside, any pose and field of
   view, ragged frames), the default kernel table and, for every fourth scene, 32x8 tiles forced;
   a third of the scenes through render_band with the adaptive tile order, the rest row-major;
+  every seventh with random per-sphere texture slots (the "all textures" extension);
 * GLSL mode: `glsl_scenes.random_uniforms` (3-60 walls, 0-3 lights, 0-11 balls, a quarter with a
   wide field of view) through the ordered kernel (adaptive tile order, wall cull), and every
   second scene through the row-major kernel (draw_image) as well;
@@ -178,14 +179,22 @@ def test_sphere_sweep(built, floor):
     import oracle
     import sfrt
     from test_gpu_parity import _fuzz_scene, diff_report
+    import scenes
     bad, pixels = [], 0
+    tex = scenes.load_all_textures()  # slot 0 is the floor (the reference's textures[0])
     with sfrt.World(0) as world:
-        world.load_texture(*floor)
+        for slot, (rgba, tw, th) in enumerate(tex):
+            world.load_texture(rgba, tw, th, slot=slot)
         for seed in range(SEED0, SEED0 + N):
             sc, w, h = _fuzz_scene(seed) if MODE == "random" else _sphere_adversarial(seed)
             w, h = SIZE or (w, h)
             world.set_option(sfrt.SFRT_OPT_RAYS_PER_LANE, 4 if seed % 4 == 0 else 0)
             world.set_scene(sc, w, h)
+            n = np.asarray(sc.spheres).shape[0]
+            # every seventh scene with the per-sphere texture slots (the "all textures" extension)
+            slots = np.random.default_rng(seed).integers(0, len(tex), n).astype(np.int32) \
+                if seed % 7 == 3 else np.zeros(n, np.int32)
+            world.set_sphere_textures(slots)
             try:
                 if seed % 3 == 1 or seed % 5 == 2:  # render_band (the adaptive tile order in use
                     b = poisoned((h, w * 4))        # from the third frame), in row bands at times
@@ -199,7 +208,13 @@ def test_sphere_sweep(built, floor):
             except sfrt.SfrtError as e:  # the kernel's march cap or texel check
                 bad.append({"seed": seed, "error": str(e)})
                 continue
-            want = oracle.Oracle.from_scene(sc, w, h, *floor).render(host_threads())
+            if seed % 7 == 3:
+                o = oracle.Oracle(w, h, sc.spheres, *tex[0], sc.cam_pos, sc.rotation, sc.hrotation,
+                                  sc.fov_h, sc.fov_v, sphere_tex=slots,
+                                  textures={k: tex[k] for k in range(1, len(tex))})
+            else:
+                o = oracle.Oracle.from_scene(sc, w, h, *floor)
+            want = o.render(host_threads())
             msg = diff_report(got, want, w)
             if msg:
                 bad.append({"seed": seed, "diff": msg})
