@@ -7,6 +7,8 @@ launch on any stream may still read it.  Queue many launches with changing
 scene state on three streams without synchronising, then compare every
 frame with the same frame rendered alone.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -366,3 +368,152 @@ def test_check_waits_for_no_other_stream(built, floor):
         g.close()
         assert hip.hipStreamDestroy(blk) == 0
     assert all(busy.values()), f"check() waited for an unrelated blocking stream: {busy}"
+
+
+def _interleaving_run(n_ops, seed, floor):
+    """Random interleavings of scene, texture and size changes with draws on five streams (two
+    at high priority, some behind queued busy work) across one sphere world, one voxel world
+    and one GLSL shader, with no host synchronisation between the calls.  Returns the list of
+    (kind, state, frame buffer) and the state pools; each frame must equal the state's frame
+    rendered alone afterwards."""
+    import sfrt
+    import torch
+    rng = np.random.default_rng(seed)
+    streams = [torch.cuda.Stream() for _ in range(3)] + [torch.cuda.Stream(priority=-1) for _ in range(2)]
+    sizes = [(160, 90), (240, 136)]
+    sph_scenes = [scenes.default10(), scenes.default10().posed(0.7, 0.3), scenes.lcg64(),
+                  scenes.Scene("lcg100", scenes.sort_spheres(scenes.lcg_spheres(99, 31)))]
+    r2 = np.random.default_rng(9)
+    textures = [floor, (r2.integers(0, 256, 64 * 64 * 4, dtype=np.uint8), 64, 64),
+                (r2.integers(0, 256, 256 * 128 * 4, dtype=np.uint8), 256, 128)]
+    vox_tex, vox_dyn = vs.load_textures()
+    vox_worlds = [vs.random_world(s)[0] for s in (3, 8, 21)]
+    vox_alt = [vox_tex[0], (r2.integers(0, 256, 32 * 32 * 4, dtype=np.uint8), 32, 32)]
+    glsl_u = [gs.random_uniforms(s, 12, 2, 6) for s in (4, 5)]
+    grounds = [floor, textures[1]]
+    world, vw, sh = sfrt.World(0), sfrt.VoxelWorld(0), sfrt.GlslShader(0)
+    state = {"sphere": [0, 0, 0], "voxel": [0, 0, 0], "glsl": [0, 0, 0]}  # scene, texture, size
+    world.load_texture(*textures[0])
+    vw.load_assets(vox_tex, vox_dyn, vs.COLORS)
+    sh.set_ground(*grounds[0])
+    sh.set_uniforms(glsl_u[0])
+    draws = []
+    try:
+        for _ in range(n_ops):
+            kind = ["sphere", "voxel", "glsl"][int(rng.integers(3))]
+            st = state[kind]
+            op = rng.random()
+            if op < 0.15:
+                st[0] = int(rng.integers(len({"sphere": sph_scenes, "voxel": vox_worlds, "glsl": glsl_u}[kind])))
+            elif op < 0.27:
+                st[1] = int(rng.integers(len({"sphere": textures, "voxel": vox_alt, "glsl": grounds}[kind])))
+                if kind == "sphere":
+                    world.load_texture(*textures[st[1]])
+                elif kind == "voxel":
+                    vw.load_texture(0, *vox_alt[st[1]])
+                else:
+                    sh.set_ground(*grounds[st[1]])
+                continue
+            elif op < 0.35:
+                st[2] = int(rng.integers(len(sizes)))
+            elif op < 0.42:
+                with torch.cuda.stream(streams[int(rng.integers(len(streams)))]):
+                    torch.cuda._sleep(int(rng.integers(1, 8)) * 1_000_000)
+                continue
+            w, h = sizes[st[2]]
+            s = streams[int(rng.integers(len(streams)))]
+            buf = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
+            with torch.cuda.stream(s):  # the poison on the draw's own stream, ahead of it
+                buf.fill_(0xA5)
+            if kind == "sphere":
+                world.set_scene(sph_scenes[st[0]], w, h)
+                world.render_band(buf.data_ptr(), w * 4, 0, h, s.cuda_stream)
+            elif kind == "voxel":
+                vw.set_scene(vox_worlds[st[0]], w, h)
+                vw.render_band(buf.data_ptr(), w * 4, 0, h, s.cuda_stream)
+            else:
+                sh.set_uniforms(glsl_u[st[0]])
+                sh.draw(buf.data_ptr(), w, h, w * 4, 0, h, s.cuda_stream)
+            draws.append((kind, tuple(st), buf, s))
+        torch.cuda.synchronize()
+        for s in streams:
+            world.check(s.cuda_stream)
+            vw.check(s.cuda_stream)
+            sh.check(s.cuda_stream)
+    finally:
+        torch.cuda.synchronize()
+        world.close()
+        vw.close()
+        sh.close()
+    pools = dict(sizes=sizes, sph_scenes=sph_scenes, textures=textures, vox_tex=vox_tex,
+                 vox_dyn=vox_dyn, vox_worlds=vox_worlds, vox_alt=vox_alt, glsl_u=glsl_u,
+                 grounds=grounds)
+    return draws, pools
+
+
+def _interleaving_want(kind, st, p):
+    """The frame of one state, rendered alone by a fresh object."""
+    import sfrt
+    w, h = p["sizes"][st[2]]
+    if kind == "sphere":
+        with sfrt.World(0) as r:
+            r.load_texture(*p["textures"][st[1]])
+            r.set_scene(p["sph_scenes"][st[0]], w, h)
+            return r.render()
+    if kind == "voxel":
+        r = sfrt.VoxelWorld(0)
+        try:
+            tex = list(p["vox_tex"])
+            tex[0] = p["vox_alt"][st[1]]
+            r.load_assets(tex, p["vox_dyn"], vs.COLORS)
+            r.set_scene(p["vox_worlds"][st[0]], w, h)
+            return r.render()
+        finally:
+            r.close()
+    r = sfrt.GlslShader(0)
+    try:
+        r.set_ground(*p["grounds"][st[1]])
+        r.set_uniforms(p["glsl_u"][st[0]])
+        return r.draw_image(w, h)
+    finally:
+        r.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_interleavings(built, floor, seed):
+    """The stream-ordering machinery under random schedules (sfrt_host.h TableSlot /
+    SharedBuffer / PinnedStage, sfrt_sched.h TileChains, the sphere world's texture atlas):
+    every frame equals its state's frame rendered alone."""
+    draws, pools = _interleaving_run(160, seed, floor)
+    kinds = {k for k, _, _, _ in draws}
+    states = {(k, st) for k, st, _, _ in draws}
+    print(f"{len(draws)} draws, {len(states)} states, {len({id(s) for *_, s in draws})} streams")
+    assert len(draws) >= 80 and kinds == {"sphere", "voxel", "glsl"} and len(states) >= 12
+    cache = {}
+    for i, (kind, st, buf, _) in enumerate(draws):
+        if (kind, st) not in cache:
+            cache[(kind, st)] = _interleaving_want(kind, st, pools)
+        want = cache[(kind, st)]
+        got = buf.cpu().numpy().ravel()
+        assert np.array_equal(got, want), f"draw {i} ({kind}, state {st}): " \
+                                          f"{_report(got, want, pools['sizes'][st[2]][0])}"
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.environ.get("SFRT_INTERLEAVE_SEEDS"),
+                    reason="on demand: SFRT_INTERLEAVE_SEEDS=<n> (400 operations per seed)")
+def test_random_interleavings_long(built, floor):
+    """test_random_interleavings over SFRT_INTERLEAVE_SEEDS seeds of 400 operations each."""
+    total = 0
+    for seed in range(100, 100 + int(os.environ["SFRT_INTERLEAVE_SEEDS"])):
+        draws, pools = _interleaving_run(400, seed, floor)
+        cache = {}
+        for i, (kind, st, buf, _) in enumerate(draws):
+            if (kind, st) not in cache:
+                cache[(kind, st)] = _interleaving_want(kind, st, pools)
+            got = buf.cpu().numpy().ravel()
+            assert np.array_equal(got, cache[(kind, st)]), f"seed {seed} draw {i} ({kind}, {st})"
+        total += len(draws)
+        print(f"seed {seed}: {len(draws)} draws, {len(cache)} states, all equal", flush=True)
+    print(f"{total} draws in all")
