@@ -321,3 +321,46 @@ def test_voxel_sweep(built):
     RESULTS["voxel"]["texel_outside_both_sides"] = ub  # reference UB, stand-in texel on both
     _record_flush()
     assert not bad, bad[:3]
+
+
+def test_multi_sweep(built, floor):
+    """The one-process multi-GPU object (sfrt_multi, devices listed twice or more on cuda:0: the
+    peer-copy transport) on random scenes: 2-4 ranks, random band rows (sfrt_multi_set_bands) that
+    change from frame to frame (band buffers grow and are retired), RGBA or packed transfers;
+    every gathered frame equals the restatement's."""
+    import oracle
+    import sfrt
+    from test_gpu_parity import _fuzz_scene, diff_report
+    rng = np.random.default_rng(SEED0 + 7)
+    bad, pixels = [], 0
+    n_multi = max(1, N // 10)  # each scene renders on several worlds
+    objs = {}
+    try:
+        for seed in range(SEED0, SEED0 + n_multi):
+            sc, w, h = _fuzz_scene(seed) if MODE == "random" else _sphere_adversarial(seed)
+            w, h = SIZE or (w, h)
+            ranks = int(rng.integers(2, 5))
+            if ranks not in objs:
+                objs[ranks] = sfrt.Multi([0] * ranks, sfrt.SFRT_MULTI_PEER)
+                objs[ranks].load_texture(*floor)
+            m = objs[ranks]
+            m.set_scene(sc, w, h)
+            if h >= ranks and rng.random() < 0.7:
+                cuts = np.sort(rng.choice(np.arange(1, h), ranks - 1, replace=False))
+                rows = np.diff(np.concatenate([[0], cuts, [h]])).astype(int).tolist()
+                m.set_bands(rows)
+            else:
+                m.set_bands(None)  # the equal split
+            m.set_transfer(int(rng.choice([sfrt.SFRT_TRANSFER_AUTO, sfrt.SFRT_TRANSFER_RGBA])))
+            got = m.update_image()
+            want = oracle.Oracle.from_scene(sc, w, h, *floor).render(host_threads())
+            msg = diff_report(got, want, w)
+            if msg:
+                bad.append({"seed": seed, "ranks": ranks, "diff": msg})
+            pixels += w * h
+            _progress("multi", seed - SEED0 + 1, bad)
+    finally:
+        for m in objs.values():
+            m.close()
+    _record("multi", n_multi, pixels, bad)
+    assert not bad, bad[:3]
