@@ -6,12 +6,15 @@ tests use, every frame against the CPU restatement byte for byte --
   kernel switch, cameras at centres / inside / near surfaces / outside, any pose and field of
   view, ragged frames), the default kernel table and, for every fourth scene, 32x8 tiles forced;
   a third of the scenes through render_band with the adaptive tile order, the rest row-major;
-  every seventh with random per-sphere texture slots (the "all textures" extension);
+  every seventh with random per-sphere texture slots (the "all textures" extension), every sixth
+  drawn as an UpdateImage pixel subset on a poisoned canvas;
 * GLSL mode: `glsl_scenes.random_uniforms` (3-60 walls, 0-3 lights, 0-11 balls, a quarter with a
   wide field of view) through the ordered kernel (adaptive tile order, wall cull), and every
-  second scene through the row-major kernel (draw_image) as well;
+  second scene through the row-major kernel (draw_image) as well; every fourth scene is instead
+  the reference's own world after 0-600 UpdateWorld steps, in any pose;
 * voxel World: `voxel_scenes.random_world` (grids, billboards, lights and shadows, view distances),
-  every second scene with the adaptive tile order.
+  every second scene with the adaptive tile order; every fourth scene is instead the reference's
+  default world seen from a random empty cell.
 
 Every fifth scene is drawn as 2-4 random row bands (global row indices, as the multi-GPU bands).
 The summary (scenes, pixels and mismatches per renderer) goes to $SFRT_PARITY_SWEEP_OUT
@@ -203,6 +206,11 @@ def test_sphere_sweep(built, floor):
                             world.render_band(b[r0].data_ptr(), w * 4, r0, n, 0)
                     world.check(0)
                     got = b.cpu().numpy().ravel()
+                elif seed % 6 == 5:  # an UpdateImage pixel subset on a poisoned canvas
+                    sub = np.random.default_rng(seed + 5).integers(1, 5, 2)
+                    got = np.full(w * h * 4, 0xA5, np.uint8)
+                    subset = (int(seed % int(sub[0])), int(sub[0]), int(seed % int(sub[1])), int(sub[1]))
+                    world.update_image(got, *subset)
                 else:  # update_image: row-major
                     got = world.render()
             except sfrt.SfrtError as e:  # the kernel's march cap or texel check
@@ -214,7 +222,11 @@ def test_sphere_sweep(built, floor):
                                   textures={k: tex[k] for k in range(1, len(tex))})
             else:
                 o = oracle.Oracle.from_scene(sc, w, h, *floor)
-            want = o.render(host_threads())
+            if seed % 6 == 5 and seed % 3 != 1 and seed % 5 != 2:
+                want = np.full(w * h * 4, 0xA5, np.uint8)
+                o.update_image(want, *subset)
+            else:
+                want = o.render(host_threads())
             msg = diff_report(got, want, w)
             if msg:
                 bad.append({"seed": seed, "diff": msg})
@@ -229,13 +241,22 @@ def test_glsl_sweep(built, floor):
     import sfrt
     rng = np.random.default_rng(SEED0)
     bad, pixels, skipped = [], 0, 0
+    sw = gs.ShaderWorld(0)  # the constructor's world, then UpdateWorld steps (Source.cpp:129)
+    world_frames = []
+    for _ in range(600):
+        world_frames.append(sw.uniforms(16, 16))
+        sw.update_world()
     s = sfrt.GlslShader(0)
     try:
         s.set_ground(*floor)
         for seed in range(SEED0, SEED0 + N):
             nw, nl, nb = int(rng.integers(3, 61)), int(rng.integers(0, 4)), int(rng.integers(0, 12))
             w, h = SIZE or [(160, 90), (96, 64), (133, 47)][seed % 3]
-            if MODE == "random":
+            if seed % 4 == 1:  # the reference's own world after k UpdateWorld steps, any pose
+                u = world_frames[int(rng.integers(0, len(world_frames)))].copy()
+                u["rotation"] = (np.float32(rng.uniform(0, 6.28)), np.float32(rng.uniform(-0.6, 0.6)))
+                u["size"] = (np.float32(w), np.float32(h))
+            elif MODE == "random":
                 u = gs.random_uniforms(seed, nw, nl, nb, w, h)
             else:
                 u, nw = _glsl_adversarial(seed, w, h)
@@ -286,7 +307,18 @@ def test_voxel_sweep(built):
     try:
         v.load_assets(tex, dyn, vs.COLORS)
         for seed in range(SEED0, SEED0 + N):
-            scene, w, h = vs.random_world(seed) if MODE == "random" else _voxel_adversarial(seed)
+            if seed % 4 == 1:  # the reference's default world from a random empty cell and pose
+                r4 = np.random.default_rng(seed)
+                blocks = vs.default_blocks()
+                while True:
+                    c = (int(r4.integers(1, 99)), int(r4.integers(1, 9)), int(r4.integers(1, 99)))
+                    if blocks[c] == vs.EMPTY:
+                        break
+                scene = vs.default_world(tuple(float(F(c[k] + r4.uniform(0.05, 0.95))) for k in range(3)),
+                                         float(r4.uniform(0, 6.28)), float(r4.uniform(-0.6, 0.6)))
+                w, h = [(320, 180), (256, 144), (333, 187)][seed % 3]
+            else:
+                scene, w, h = vs.random_world(seed) if MODE == "random" else _voxel_adversarial(seed)
             w, h = SIZE or (w, h)
             v.set_option(sfrt.SFRT_OPT_TILE_ORDER, seed % 2)  # off by default; on: LPT order
             v.set_scene(scene, w, h)
