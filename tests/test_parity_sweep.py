@@ -16,10 +16,14 @@ tests use, every frame against the CPU restatement byte for byte --
   every second scene with the adaptive tile order; every fourth scene is instead the reference's
   default world seen from a random empty cell.
 
+* the multi-GPU object (sfrt_multi): N / 10 sphere scenes over 2-4 ranks on cuda:0.
+
 Every fifth scene is drawn as 2-4 random row bands (global row indices, as the multi-GPU bands).
-The summary (scenes, pixels and mismatches per renderer) goes to $SFRT_PARITY_SWEEP_OUT
-(profiles/r6ps_parity_sweep.json is one such run).
-    SFRT_PARITY_SWEEP=1000 python -m pytest tests/test_parity_sweep.py -m gpu
+SFRT_PARITY_SWEEP_MODE=adversarial pushes each generator to its degenerate corners;
+SFRT_PARITY_SWEEP_SIZE=WxH draws every scene at that size.  The summary (scenes, pixels and
+mismatches per renderer) goes to $SFRT_PARITY_SWEEP_OUT (profiles/r6ps_*, r6pa_*, r6p1_*, r6p4_*,
+r6pm_* are such runs).
+    SFRT_PARITY_SWEEP=1000 python -m pytest tests/test_parity_sweep.py -m gpu -s
 """
 import json
 import os
