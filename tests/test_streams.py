@@ -529,3 +529,57 @@ def test_random_interleavings_long(built, floor):
         total += len(draws)
         print(f"seed {seed}: {len(draws)} draws, {len(cache)} states, all equal", flush=True)
     print(f"{total} draws in all")
+
+
+@pytest.mark.gpu
+def test_random_display_pipeline(built, floor):
+    """The display path (submit_frame / wait_frame into pinned host frames, two in flight) under
+    random scene, size and texture changes between submissions: the pipeline slots grow with the
+    frame and the record ring with the sphere count; every delivered frame equals its state's
+    frame rendered alone."""
+    import sfrt
+    rng = np.random.default_rng(77)
+    sizes = [(160, 90), (320, 180), (240, 136)]
+    sph_scenes = [scenes.default10(), scenes.lcg64().posed(0.4, -0.1),
+                  scenes.Scene("lcg90", scenes.sort_spheres(scenes.lcg_spheres(89, 5)))]
+    r2 = np.random.default_rng(3)
+    textures = [floor, (r2.integers(0, 256, 128 * 64 * 4, dtype=np.uint8), 128, 64)]
+    frames = [sfrt.HostFrame(320 * 180 * 4) for _ in range(3)]
+    pending, delivered = [], []
+    st = [0, 0, 0]  # scene, texture, size
+    try:
+        with sfrt.World(0) as world:
+            world.load_texture(*textures[0])
+            for k in range(200):
+                op = rng.random()
+                if op < 0.2:
+                    st[0] = int(rng.integers(len(sph_scenes)))
+                elif op < 0.3:
+                    st[1] = int(rng.integers(len(textures)))
+                    world.load_texture(*textures[st[1]])
+                elif op < 0.45:
+                    st[2] = int(rng.integers(len(sizes)))
+                w, h = sizes[st[2]]
+                world.set_scene(sph_scenes[st[0]], w, h)
+                if len(pending) == 2:  # at most two frames in flight
+                    t, fr, s = pending.pop(0)
+                    world.wait_frame(t)
+                    delivered.append((tuple(s), fr.array[: sizes[s[2]][0] * sizes[s[2]][1] * 4].copy()))
+                fr = frames[k % 3]
+                pending.append((world.submit_frame(fr), fr, tuple(st)))
+            for t, fr, s in pending:
+                world.wait_frame(t)
+                delivered.append((tuple(s), fr.array[: sizes[s[2]][0] * sizes[s[2]][1] * 4].copy()))
+    finally:
+        for fr in frames:
+            fr.free()
+    cache = {}
+    for i, (s, got) in enumerate(delivered):
+        if s not in cache:
+            w, h = sizes[s[2]]
+            with sfrt.World(0) as ref:
+                ref.load_texture(*textures[s[1]])
+                ref.set_scene(sph_scenes[s[0]], w, h)
+                cache[s] = ref.render()
+        assert np.array_equal(got, cache[s]), f"frame {i} (state {s}): {_report(got, cache[s], sizes[s[2]][0])}"
+    assert len(delivered) == 200 and len(cache) >= 8
