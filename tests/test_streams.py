@@ -235,8 +235,8 @@ def test_growth_waits_for_no_other_stream(built, floor):
 
 @pytest.mark.gpu
 def test_destroyed_stream_is_forgotten(built, floor):
-    """A caller may destroy a stream after drawing on it (hipStreamDestroy first waits for its
-    work).  The world's tile-order chain still remembers that stream as its last one: a larger
+    """A caller may destroy a stream once its frames are done (HIP leaves work still queued on a
+    destroyed stream undefined).  The world's tile-order chain still remembers that stream as its last one: a larger
     frame on a seventeenth stream takes that chain over (sfrt_sched.h TileChains: sixteen chains,
     the least recently used one taken over) and reallocates its buffers.  Neither may pass the
     dead handle to HIP (a call on it crashed, profiles/r6y_dead_stream.txt), and the frames equal
