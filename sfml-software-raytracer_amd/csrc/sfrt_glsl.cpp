@@ -125,7 +125,13 @@ struct sfrt_glsl {
   int* d_status = nullptr;
   uint32_t* d_frame = nullptr;
   size_t d_frame_px = 0;
+  sfrt::Relay relay;         // events recorded on callers' streams, relayed (sfrt_host.h)
   std::mutex mu;
+
+  sfrt_glsl() {
+    for (auto& t : slots) t.relay = &relay;
+    ground.relay = &relay;
+  }
 
   ~sfrt_glsl() {
     sfrt::DeviceGuard g(device);
@@ -136,6 +142,7 @@ struct sfrt_glsl {
     mip_stage.release();
     ground.release();
     for (auto& t : slots) t.release();
+    relay.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
     if (stream) (void)hipStreamDestroy(stream);
@@ -321,7 +328,7 @@ struct sfrt_glsl {
   // The current table slot's event, for the launch that reads it to record (its stop event:
   // sfrt_host.h TableSlot::launch_event), and the slot marked busy once that launch is queued.
   void* launch_event() const { return slots[cur_slot].launch_event(); }
-  void launched(hipStream_t s) { slots[cur_slot].launched_with(s); }
+  hipError_t launched(hipStream_t s) { return slots[cur_slot].launched_with(s); }
 
   // On s itself: hipMemcpy / hipMemset run on the null stream, which also waits for every blocking
   // stream of the process (a caller's hipStreamCreate streams), not just s.
@@ -498,7 +505,7 @@ int sfrt_glsl_draw(sfrt_glsl* g, void* dev_pixels, int width, int height, int64_
   const bool queued = sfrt::launch_glsl(f, s, g->launch_event()) == 0;
   HIP_TRY(sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;
-  g->launched(s);
+  HIP_TRY(g->launched(s));
   return SFRT_OK;
 }
 
@@ -526,7 +533,7 @@ int sfrt_glsl_draw_image(sfrt_glsl* g, uint8_t* pixels, int width, int height) {
   f.out = g->d_frame;
   f.out_pitch = width;
   if (sfrt::launch_glsl(f, g->stream, g->launch_event())) return SFRT_E_HIP;
-  g->launched(g->stream);
+  HIP_TRY(g->launched(g->stream));
   HIP_TRY(hipMemcpyAsync(pixels, g->d_frame, px * 4, hipMemcpyDeviceToHost, g->stream));
   return g->read_status(g->stream);
 }

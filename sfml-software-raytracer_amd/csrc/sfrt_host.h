@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -50,6 +52,47 @@ struct DeviceGuard {
   DeviceGuard& operator=(const DeviceGuard&) = delete;
 };
 
+// Events recorded on a caller's stream are not used once the call returns: HIP's event calls read
+// the stream an event was last recorded on, and a caller may destroy that stream once its frames
+// are done (hipEventSynchronize on an event last recorded on a destroyed stream returned
+// hipErrorStreamCaptureUnsupported now and then, tests/test_streams.py
+// test_random_interleavings_long).  So each such event is relayed at once, while the caller's
+// stream is alive, to an event recorded on a stream the object owns, which completes after it;
+// only relayed events are waited on later.
+struct Relay {
+  hipStream_t stream = nullptr;
+  hipEvent_t scratch = nullptr;
+  hipError_t ensure() {
+    hipError_t e;
+    if (!stream && (e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess) return e;
+    if (!scratch && (e = hipEventCreateWithFlags(&scratch, hipEventDisableTiming)) != hipSuccess) return e;
+    return hipSuccess;
+  }
+  // `to` completes after `from`, recorded just now on a caller's stream.
+  hipError_t pass(hipEvent_t from, hipEvent_t to) {
+    hipError_t e;
+    if ((e = ensure()) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(stream, from, 0)) != hipSuccess) return e;
+    return hipEventRecord(to, stream);
+  }
+  // `to` completes after the work queued on s so far.
+  hipError_t record(hipStream_t s, hipEvent_t to) {
+    hipError_t e;
+    if ((e = ensure()) != hipSuccess) return e;
+    if ((e = hipEventRecord(scratch, s)) != hipSuccess) return e;
+    return pass(scratch, to);
+  }
+  void release() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    if (scratch) (void)hipEventDestroy(scratch);
+    stream = nullptr;
+    scratch = nullptr;
+  }
+};
+
 // One slot of a per-frame table ring (sfrt_voxel.cpp, sfrt_glsl.cpp): device tables, their
 // pinned staging copy, and one event that every earlier user of the slot -- the staging copy and
 // each launch that read it, on whatever stream -- completes before.  A launch on another stream
@@ -60,18 +103,20 @@ struct TableSlot {
   void* d = nullptr;
   void* h = nullptr;
   size_t cap = 0;
-  hipEvent_t ev = nullptr;
-  hipStream_t last = nullptr;  // stream of the last record of ev (valid while pending)
+  hipEvent_t ev = nullptr;     // relayed (Relay): completes after every earlier user
+  hipEvent_t stop = nullptr;   // the launch's own stop event, on the caller's stream
+  hipStream_t last = nullptr;  // stream of the last user (compared only, valid while pending)
   bool pending = false;
+  Relay* relay = nullptr;      // the owner's (set at its creation)
 
   // Before restaging: every earlier user has finished with the slot.
   hipError_t reclaim() {
-    if (pending) {
-      const hipError_t e = hipEventSynchronize(ev);
-      if (e != hipSuccess) return e;
-    }
+    hipError_t e;
+    if (pending && (e = hipEventSynchronize(ev)) != hipSuccess) return e;
     pending = false;
-    return ev ? hipSuccess : hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!stop && (e = hipEventCreateWithFlags(&stop, hipEventDisableTiming)) != hipSuccess) return e;
+    return hipSuccess;
   }
   // After the staging copy was queued on s (a later reader on another stream waits for it).
   hipError_t staged(hipStream_t s) { return mark(s); }
@@ -102,18 +147,22 @@ struct TableSlot {
   // (hipExtLaunchKernelGGL: the dispatch packet's own completion signal records it, so no marker
   // packet sits between two frames -- a hipEventRecord after every launch cost the 1080p voxel
   // frame ~5 us, profiles/ab/r6_ab3), then launched_with(s) once the launch is queued on s.
-  hipEvent_t launch_event() const { return ev; }
-  void launched_with(hipStream_t s) {
+  hipEvent_t launch_event() const { return stop; }
+  hipError_t launched_with(hipStream_t s) {
+    const hipError_t e = relay->pass(stop, ev);
+    if (e != hipSuccess) return e;
     last = s;
     pending = true;
+    return hipSuccess;
   }
   void release() {
     (void)hipFree(d);
     (void)hipHostFree(h);
     retired.release();
     if (ev) (void)hipEventDestroy(ev);
+    if (stop) (void)hipEventDestroy(stop);
     d = h = nullptr;
-    ev = nullptr;
+    ev = stop = nullptr;
     cap = 0;
     pending = false;
   }
@@ -121,7 +170,7 @@ struct TableSlot {
  private:
   RetiredHost retired;
   hipError_t mark(hipStream_t s) {
-    const hipError_t e = hipEventRecord(ev, s);
+    const hipError_t e = relay->record(s, ev);
     if (e != hipSuccess) return e;
     last = s;
     pending = true;
@@ -138,9 +187,10 @@ struct TableSlot {
 // rewrite, orders the first later launch on each other stream after it.  (A second event recorded
 // after every launch, one per reading stream, had cost the 1080p voxel frame 5 us: ab/r6_ab3.)
 struct SharedBuffer {
-  hipEvent_t written = nullptr;
-  hipStream_t writer = nullptr;
+  hipEvent_t written = nullptr;  // relayed (Relay): the rewrite may run on a caller's stream
+  hipStream_t writer = nullptr;  // compared only
   bool have_written = false;
+  Relay* relay = nullptr;        // the owner's (set at its creation)
   std::vector<hipStream_t> current;  // other streams already ordered after the last rewrite
 
   // Before queuing a launch on s that reads the buffer.
@@ -174,7 +224,7 @@ struct SharedBuffer {
     hipError_t e;
     if (!written && (e = hipEventCreateWithFlags(&written, hipEventDisableTiming)) != hipSuccess)
       return e;
-    if ((e = hipEventRecord(written, w)) != hipSuccess) return e;
+    if ((e = relay->record(w, written)) != hipSuccess) return e;
     writer = w;
     have_written = true;
     current.clear();
@@ -191,6 +241,7 @@ struct SharedBuffer {
 // Pinned staging for a stream-ordered upload from the caller's (pageable) memory: the bytes are
 // copied into the staging buffer on the host, then to the device on a stream; the buffer is reused
 // only after its last device copy has run (a host wait on that copy alone, never on the device).
+// The copy runs on a stream the owner keeps alive (its own): `ev` is waited on later (Relay).
 struct PinnedStage {
   void* h = nullptr;
   size_t cap = 0;
@@ -244,8 +295,21 @@ struct PinnedStage {
 
 }  // namespace sfrt
 
+namespace sfrt {
+// With SFRT_DEBUG set in the environment, a failing HIP call names itself on stderr (the ABI
+// returns only SFRT_E_HIP).
+inline void report_hip_error(hipError_t e, const char* expr, const char* file, int line) {
+  static const bool on = std::getenv("SFRT_DEBUG") != nullptr;
+  if (on) std::fprintf(stderr, "sfrt: %s:%d: %s -> %s\n", file, line, expr, hipGetErrorName(e));
+}
+}  // namespace sfrt
+
 // Any HIP failure becomes SFRT_E_HIP at the boundary.
-#define HIP_TRY(expr)                            \
-  do {                                           \
-    if ((expr) != hipSuccess) return SFRT_E_HIP; \
+#define HIP_TRY(expr)                                                 \
+  do {                                                                \
+    const hipError_t hip_try_e = (expr);                              \
+    if (hip_try_e != hipSuccess) {                                    \
+      sfrt::report_hip_error(hip_try_e, #expr, __FILE__, __LINE__);   \
+      return SFRT_E_HIP;                                              \
+    }                                                                 \
   } while (0)

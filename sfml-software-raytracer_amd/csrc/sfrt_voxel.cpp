@@ -154,7 +154,13 @@ struct sfrt_voxel {
   size_t d_frame_px = 0;
   int tile_order_on = 0;     // SFRT_OPT_TILE_ORDER: off by default here (slower)
   sfrt::TileChains scheds;   // adaptive tile order (sfrt_sched.h), render_band; one chain per stream
+  sfrt::Relay relay;         // events recorded on callers' streams, relayed (sfrt_host.h)
   std::mutex mu;
+
+  sfrt_voxel() {
+    for (auto& t : slots) t.relay = &relay;
+    shared.relay = &relay;
+  }
 
   ~sfrt_voxel() {
     sfrt::DeviceGuard g(device);
@@ -174,6 +180,7 @@ struct sfrt_voxel {
     shared.release();
     tex_stage.release();
     for (auto& t : slots) t.release();
+    relay.release();
     (void)hipFree(d_status);
     (void)hipFree(d_frame);
     if (stream) (void)hipStreamDestroy(stream);
@@ -325,7 +332,7 @@ struct sfrt_voxel {
     // would see them: the box covers them too while they may hold codes
     const int bx = std::max(nx, box[0]), by = std::max(ny, box[1]), bz = std::max(nz, box[2]);
     if (sfrt::launch_voxel_cells(d_cells, c.d, nx, ny, nz, bx, by, bz, s)) return SFRT_E_HIP;
-    HIP_TRY(hipEventRecord(c.ev, s));
+    HIP_TRY(relay.record(s, c.ev));  // s may be a caller's stream
     c.pending = true;
     stage_next ^= 1;
     HIP_TRY(shared.after_write(s));
@@ -382,7 +389,7 @@ struct sfrt_voxel {
   // the slot marked busy once that launch is queued on s (the event also covers the launch's
   // read of the grid: SharedBuffer).
   void* launch_event() const { return slots[cur_slot].launch_event(); }
-  void launched(hipStream_t s) { slots[cur_slot].launched_with(s); }
+  hipError_t launched(hipStream_t s) { return slots[cur_slot].launched_with(s); }
 
   // On s itself: hipMemcpy / hipMemset run on the null stream, which also waits for every blocking
   // stream of the process (a caller's hipStreamCreate streams), not just s.
@@ -539,7 +546,7 @@ int sfrt_voxel_update_image(sfrt_voxel* v, uint8_t* pixels, int ystart, int yadd
   f.out = v->d_frame;
   f.out_pitch = sub_w;
   if (sfrt::launch_voxel(f, v->stream, v->launch_event())) return SFRT_E_HIP;
-  v->launched(v->stream);
+  HIP_TRY(v->launched(v->stream));
   std::vector<uint32_t> stage(px);
   HIP_TRY(hipMemcpyAsync(stage.data(), v->d_frame, px * 4, hipMemcpyDeviceToHost, v->stream));
   rc = v->read_status(v->stream);
@@ -583,7 +590,7 @@ int sfrt_voxel_render_band(sfrt_voxel* v, void* dev_pixels, int64_t pitch_bytes,
   const bool queued = sfrt::launch_voxel(f, s, v->launch_event()) == 0;
   HIP_TRY(sched.end(p, s, queued));
   if (!queued) return SFRT_E_HIP;
-  v->launched(s);
+  HIP_TRY(v->launched(s));
   return SFRT_OK;
 }
 

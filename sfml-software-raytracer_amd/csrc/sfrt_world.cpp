@@ -150,7 +150,9 @@ struct sfrt_world {
   static constexpr int kRing = 8;
   sfrt::SphereRec* d_spheres[kRing] = {};
   sfrt::SphereRec* h_spheres[kRing] = {};
-  hipEvent_t spheres_ev[kRing] = {};
+  hipEvent_t spheres_ev[kRing] = {};    // relayed (sfrt_host.h Relay): the slot's last reader done
+  hipEvent_t spheres_stop[kRing] = {};  // that reader's own stop event, on the caller's stream
+  sfrt::Relay relay;
   bool spheres_pending[kRing] = {};
   int d_spheres_cap = 0;
   int ring = 0;
@@ -200,7 +202,9 @@ struct sfrt_world {
       (void)hipFree(d_spheres[k]);
       (void)hipHostFree(h_spheres[k]);
       if (spheres_ev[k]) (void)hipEventDestroy(spheres_ev[k]);
+      if (spheres_stop[k]) (void)hipEventDestroy(spheres_stop[k]);
     }
+    relay.release();
     (void)hipFree(d_frame);
     (void)hipHostFree(h_stage);
     retired_host.release();
@@ -313,6 +317,7 @@ struct sfrt_world {
       HIP_TRY(hipHostMalloc(&h_spheres[k], sizeof(sfrt::SphereRec) * (size_t)cap,
                             hipHostMallocDefault));
       if (!spheres_ev[k]) HIP_TRY(hipEventCreateWithFlags(&spheres_ev[k], hipEventDisableTiming));
+      if (!spheres_stop[k]) HIP_TRY(hipEventCreateWithFlags(&spheres_stop[k], hipEventDisableTiming));
     }
     d_spheres_cap = cap;
     return SFRT_OK;
@@ -343,7 +348,7 @@ struct sfrt_world {
   // After the launch that reads the staged slot has been queued on s.
   int launched(hipStream_t s) {
     if (staged < 0) return SFRT_OK;
-    HIP_TRY(hipEventRecord(spheres_ev[staged], s));
+    HIP_TRY(relay.record(s, spheres_ev[staged]));
     spheres_pending[staged] = true;
     staged = -1;
     return SFRT_OK;
@@ -351,11 +356,13 @@ struct sfrt_world {
   // The same through the launch itself: the staged slot's event for launch_trace to record as
   // the kernel's stop event (no marker packet between frames, sfrt_host.h
   // TableSlot::launch_event), then launched_with() once the launch is queued.
-  void* ring_event() const { return staged >= 0 ? spheres_ev[staged] : nullptr; }
-  void launched_with() {
-    if (staged < 0) return;
+  void* ring_event() const { return staged >= 0 ? spheres_stop[staged] : nullptr; }
+  int launched_with() {
+    if (staged < 0) return SFRT_OK;
+    HIP_TRY(relay.pass(spheres_stop[staged], spheres_ev[staged]));
     spheres_pending[staged] = true;
     staged = -1;
+    return SFRT_OK;
   }
 
   // Before a render_band / submit_frame launch on s: link f into the tile-order chain.
@@ -501,6 +508,7 @@ int sfrt_world_create(int hip_device, sfrt_world** out) {
     return SFRT_E_HIP;
   sfrt_world* w = new sfrt_world();
   w->device = hip_device;
+  w->tex_written.relay = &w->relay;
   // Camera defaults (SphereWorld.h:10-21) and the constructor's conversion (:72-73).
   w->cam.fov_h = sfrt_deg_to_rad(75.0f);
   w->cam.fov_v = sfrt_deg_to_rad(47.0f);
@@ -754,7 +762,7 @@ int sfrt_world_update_image(sfrt_world* w, uint8_t* pixels, int ystart, int yadd
   rc = w->stage_spheres(f, recs, w->stream, false);
   if (rc) return rc;
   if (sfrt::launch_trace(f, recs.data(), w->stream, nullptr, w->ring_event())) return SFRT_E_HIP;
-  w->launched_with();
+  if ((rc = w->launched_with())) return rc;
   HIP_TRY(hipMemcpyAsync(w->h_stage, w->d_frame, px * 4, hipMemcpyDeviceToHost, w->stream));
   rc = w->read_status(w->stream);
   if (rc) return rc;
@@ -804,7 +812,7 @@ int sfrt_world_render_band(sfrt_world* w, void* dev_pixels, int64_t pitch_bytes,
   if ((rc = w->sched_begin(f, s))) return rc;
   if ((rc = w->sched_end(f, s, sfrt::launch_trace(f, recs.data(), s, nullptr, w->ring_event()) == 0)))
     return rc;
-  w->launched_with();
+  if ((rc = w->launched_with())) return rc;
   return SFRT_OK;
 }
 
@@ -958,7 +966,7 @@ int sfrt_world_submit_frame(sfrt_world* w, uint8_t* pixels, int64_t* ticket) {
   if ((rc = w->sched_end(f, w->stream,
                          sfrt::launch_trace(f, recs.data(), w->stream, nullptr, w->ring_event()) == 0)))
     return rc;
-  w->launched_with();
+  if ((rc = w->launched_with())) return rc;
   HIP_TRY(hipEventRecord(slot.rendered, w->stream));
   HIP_TRY(hipStreamWaitEvent(w->copy_stream, slot.rendered, 0));
   HIP_TRY(hipMemcpyAsync(pixels, slot.d_buf, px * 4, hipMemcpyDeviceToHost, w->copy_stream));

@@ -372,12 +372,16 @@ def test_check_waits_for_no_other_stream(built, floor):
 
 def _interleaving_run(n_ops, seed, floor):
     """Random interleavings of scene, texture and size changes with draws on five streams (two
-    at high priority, some behind queued busy work) across one sphere world, one voxel world
+    at high priority, some behind queued busy work) and on short-lived streams (one in ten
+    draws: created, drained and destroyed -- past sixteen streams an object's chains are taken
+    over, sfrt_sched.h) across one sphere world, one voxel world
     and one GLSL shader, with no host synchronisation between the calls.  Returns the list of
     (kind, state, frame buffer) and the state pools; each frame must equal the state's frame
     rendered alone afterwards."""
+    import ctypes
     import sfrt
     import torch
+    hip = ctypes.CDLL("libamdhip64.so")
     rng = np.random.default_rng(seed)
     streams = [torch.cuda.Stream() for _ in range(3)] + [torch.cuda.Stream(priority=-1) for _ in range(2)]
     sizes = [(160, 90), (240, 136)]
@@ -433,7 +437,13 @@ def _interleaving_run(n_ops, seed, floor):
                     host = sh.draw_image(w, h)
                 draws.append((kind, tuple(st), host, None))
                 continue
-            s = streams[int(rng.integers(len(streams)))]
+            raw = None
+            if rng.random() < 0.1:  # a short-lived stream: created, drawn on, drained, destroyed
+                raw = ctypes.c_void_p()
+                assert hip.hipStreamCreateWithFlags(ctypes.byref(raw), 1) == 0
+                s = torch.cuda.ExternalStream(raw.value)
+            else:
+                s = streams[int(rng.integers(len(streams)))]
             buf = torch.empty((h, w * 4), dtype=torch.uint8, device="cuda:0")
             with torch.cuda.stream(s):  # the poison on the draw's own stream, ahead of it
                 buf.fill_(0xA5)
@@ -447,6 +457,8 @@ def _interleaving_run(n_ops, seed, floor):
                 sh.set_uniforms(glsl_u[st[0]])
                 sh.draw(buf.data_ptr(), w, h, w * 4, 0, h, s.cuda_stream)
             draws.append((kind, tuple(st), buf, s))
+            if raw is not None:  # the objects remember it as a chain's last stream, by handle only
+                assert hip.hipStreamSynchronize(raw) == 0 and hip.hipStreamDestroy(raw) == 0
         torch.cuda.synchronize()
         for s in streams:
             world.check(s.cuda_stream)
@@ -518,7 +530,8 @@ def test_random_interleavings(built, floor, seed):
 def test_random_interleavings_long(built, floor):
     """test_random_interleavings over SFRT_INTERLEAVE_SEEDS seeds of 400 operations each."""
     total = 0
-    for seed in range(100, 100 + int(os.environ["SFRT_INTERLEAVE_SEEDS"])):
+    seed0 = int(os.environ.get("SFRT_INTERLEAVE_SEED0", "100"))
+    for seed in range(seed0, seed0 + int(os.environ["SFRT_INTERLEAVE_SEEDS"])):
         draws, pools = _interleaving_run(400, seed, floor)
         cache = {}
         for i, (kind, st, buf, _) in enumerate(draws):
